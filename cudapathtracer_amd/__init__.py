@@ -1,0 +1,13 @@
+"""cudapathtracer_amd -- MI355X-native (gfx950) re-authoring of CulDeVu/CUDAPathTracer's
+per-pixel path-integration loop behind a C-ABI (include/pt/pt.h, libptamd.so).
+
+Host surface (OBJ ingest, BVH build, camera, PPM) is C++ in csrc/host; the render path is
+hand-written HIP in csrc/hip.  Python here is only orchestration over ctypes.
+"""
+from ._lib import (PT_FLAG_COUNT, PT_FLAG_NO_DEAD_PATH_SKIP, PT_FLAG_NO_PRIMARY_CACHE,  # noqa: F401
+                   PT_FLAG_REFERENCE_TRAVERSAL, PT_INTEGRATOR_HEAD, PT_INTEGRATOR_UNIDIR, PtError, LIB_PATH)
+from .api import (Renderer, Scene, camera_ray, make_camera, morton_i_to_pxl, morton_pxl_to_i,  # noqa: F401
+                  tonemap_u8, write_ppm)
+
+__all__ = ["Scene", "Renderer", "make_camera", "camera_ray", "morton_pxl_to_i", "morton_i_to_pxl", "write_ppm",
+           "tonemap_u8", "PtError"]

@@ -1,0 +1,192 @@
+"""Host-side mirror of the reference's render flow (kernel.cu:565-790) over the C-ABI.
+
+    scene = Scene()
+    scene.load_obj("models/CornellBox-Original.obj", (0, 0, 0), 1)      # loadOBJ, modelLoader.h:125
+    scene.load_obj("models/teapot.obj", (0.35, 0.6, 0.3), 0.75)         # kernel.cu:591-592
+    scene.build_bvh()                                                   # buildBVH, BVH.h:443 + guard :627
+    cam = make_camera(pos=(0, 1, 3), dist_from_film=1, focal_length=3, radius=0,
+                      width=512, height=512)                            # kernel.cu:642-648
+    with Renderer(scene) as r:                                          # uploads, kernel.cu:664-700
+        img, stats = r.render(cam, 512, 512, spp=99, bounces=3)         # NUM_SAMPLES-1 samples, :709
+    write_ppm("image.ppm", img)                                         # kernel.cu:763-778
+
+Every call goes through libptamd.so; arrays returned to Python are copies of the C++ host
+scene (numpy structured views for tests) or the float32 image the gfx950 kernel wrote.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+VEC3 = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4")])
+TRI = np.dtype([("v0", "<i4"), ("v1", "<i4"), ("v2", "<i4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                ("mat", "<i4")])
+MAT = np.dtype([("albedo", "<f8", (3,)), ("emission", "<f8", (3,))])
+NODE = np.dtype([("lo", "<f4", (3,)), ("hi", "<f4", (3,)), ("left", "<u4"), ("right", "<u4")])
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    buf = C.string_at(ptr, n * dtype.itemsize)
+    return np.frombuffer(buf, dtype=dtype).copy()
+
+
+class Scene:
+    """The reference's scene globals (modelLoader.h:43-47) as an object owned by libptamd."""
+
+    def __init__(self):
+        self._h = L.lib().pt_scene_new()
+        if not self._h:
+            raise MemoryError("pt_scene_new failed")
+
+    def close(self):
+        if self._h:
+            L.lib().pt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_obj(self, path, origin=(0.0, 0.0, 0.0), scale=1.0, flip_normals=False, mtl_basepath=None):
+        """loadOBJ (modelLoader.h:125-210).  mtl_basepath=None is the reference's "models/"."""
+        o = L.Vec3(*[float(v) for v in origin])
+        L.check(L.lib().pt_scene_load_obj(self._h, str(path).encode(),
+                                          None if mtl_basepath is None else str(mtl_basepath).encode(),
+                                          o, float(scale), int(bool(flip_normals))))
+        return self
+
+    loadOBJ = load_obj
+
+    @property
+    def warning(self) -> str:
+        return (L.lib().pt_scene_last_warning(self._h) or b"").decode(errors="replace")
+
+    def build_bvh(self):
+        """buildBVH (BVH.h:443-474) + the depth guard of kernel.cu:627-631."""
+        L.check(L.lib().pt_scene_build_bvh(self._h))
+        return self
+
+    buildBVH = build_bvh
+
+    def view(self) -> L.SceneView:
+        v = L.SceneView()
+        L.check(L.lib().pt_scene_view(self._h, C.byref(v)))
+        return v
+
+    def arrays(self):
+        """Copies of verts/tris/mats/lights/bvh as numpy structured arrays (test surface)."""
+        v = self.view()
+        return dict(
+            verts=_arr(v.verts, v.num_verts, VEC3),
+            tris=_arr(v.tris, v.num_tris, TRI),
+            mats=_arr(v.mats, v.num_mats, MAT),
+            lights=_arr(v.lights, v.num_lights, np.dtype("<u4")),
+            total_light_area=np.float32(v.total_light_area),
+            bvh=_arr(v.bvh, v.bvh_size, NODE),
+            bvh_depth=int(v.bvh_depth),
+        )
+
+
+def make_camera(pos=(0.0, 1.0, 3.0), dist_from_film=1.0, focal_length=3.0, radius=0.0, width=512, height=512):
+    """camera.h:26-34 (defaults = kernel.cu:642-648)."""
+    c = L.Camera()
+    c.pos = L.Vec3(*[float(v) for v in pos])
+    c.dist_from_film = float(dist_from_film)
+    c.focal_length = float(focal_length)
+    c.radius = float(radius)
+    c.pxl_width = int(width)
+    c.pxl_height = int(height)
+    return c
+
+
+def camera_ray(cam, idx, lens=False, u1=0.0, u2=0.0):
+    o, d = L.Vec3(), L.Vec3()
+    L.lib().pt_camera_ray(C.byref(cam), int(idx), int(bool(lens)), float(u1), float(u2), C.byref(o), C.byref(d))
+    return (o.x, o.y, o.z), (d.x, d.y, d.z)
+
+
+def morton_pxl_to_i(x, y):
+    return int(L.lib().pt_morton_pxl_to_i(int(x), int(y)))
+
+
+def morton_i_to_pxl(i):
+    x, y = C.c_uint32(), C.c_uint32()
+    L.lib().pt_morton_i_to_pxl(int(i), C.byref(x), C.byref(y))
+    return x.value, y.value
+
+
+def write_ppm(path, img):
+    """kernel.cu:763-778 on a (H, W, 3) float32 or float64 mean image."""
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    if img.dtype == np.float64:
+        L.check(L.lib().pt_write_ppm_f64(str(path).encode(), img.ctypes.data, w, h))
+    else:
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        L.check(L.lib().pt_write_ppm(str(path).encode(), img.ctypes.data, w, h))
+
+
+def tonemap_u8(c):
+    return int(L.lib().pt_tonemap_u8(float(c)))
+
+
+class Renderer:
+    """Device-resident scene on one GPU (pt_create) and the render call (pt_render)."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        err = C.c_int(0)
+        self._scene_view = scene.view()
+        self._h = L.lib().pt_create(C.byref(self._scene_view), int(device), C.byref(err))
+        if not self._h:
+            L.check(err.value if err.value != 0 else L.PT_E_HIP)
+        self.device = device
+
+    def close(self):
+        if self._h:
+            L.lib().pt_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def params(width, height, spp, bounces=3, integrator=0, seed=1234, flags=0, shard_index=0, shard_count=1):
+        p = L.Params()
+        p.width, p.height, p.spp, p.bounces = int(width), int(height), int(spp), int(bounces)
+        p.integrator, p.flags, p.seed = int(integrator), int(flags), int(seed)
+        p.shard_index, p.shard_count = int(shard_index), int(shard_count)
+        return p
+
+    def render(self, cam, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0,
+               shard_index=0, shard_count=1):
+        """Returns (image float32 (H, W, 3), stats dict)."""
+        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count)
+        out = np.zeros((height, width, 3), dtype=np.float32)
+        st = L.Stats()
+        L.check(L.lib().pt_render(self._h, C.byref(p), C.byref(cam), out.ctypes.data, C.byref(st)))
+        return out, st.as_dict()
+
+    def render_device(self, cam, d_out_ptr, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0,
+                      shard_index=0, shard_count=1, stream_ptr=None):
+        """Render this shard into a caller-owned, zero-filled device buffer (e.g. a torch tensor)."""
+        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count)
+        st = L.Stats()
+        L.check(L.lib().pt_render_device(self._h, C.byref(p), C.byref(cam), C.c_void_p(int(d_out_ptr)),
+                                         None if stream_ptr is None else C.c_void_p(int(stream_ptr)), C.byref(st)))
+        return st.as_dict()

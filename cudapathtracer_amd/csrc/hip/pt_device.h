@@ -1,0 +1,376 @@
+// pt_device.h -- gfx950 device code of the path tracer: data layout in HBM, arithmetic
+// helpers, XORWOW, slab/triangle tests and the two BVH walks.
+//
+// Arithmetic contract (DESIGN.md "Arithmetic spec"): the whole library is compiled with
+// -ffp-contract=off, so every float/double expression below is evaluated as the reference's
+// C++ spells it -- IEEE single/double ops in source order, correctly rounded '/' and sqrt --
+// and matches the CPU oracle bit for bit.  Places that intentionally use FMA say so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptd {
+
+constexpr float kMaxFloat = 100000.0f;        // limits.h:3 MAX_FLOAT
+constexpr uint32_t kLeaf = 0x80000000u;       // limits.h:6 BVH_LEAF_FLAG
+constexpr int kStack = 64;                    // kernel.cu:35 MAX_BVH_DEPTH
+
+// ------------------------------------------------------------------ HBM layout
+// Both children of one reference BVH node in one 64-B record (4 x 16-B loads).  Child ref:
+// inner -> node index (same index as the reference's BFS array), leaf -> kLeaf | slot, where
+// slot is the triangle's position in left-first DFS leaf order (its tie-break rank).
+struct alignas(16) DNode {
+    float4 a;   // c0.lo.xyz, c0.hi.x
+    float4 b;   // c0.hi.yz, c1.lo.xy
+    float4 c;   // c1.lo.z, c1.hi.xyz
+    uint4 d;    // c0 ref, c1 ref, -, -
+};
+static_assert(sizeof(DNode) == 64, "node record is 64 B");
+
+// The reference's own node (BVH.h:111-115), used by the reference-order walk.
+struct alignas(16) RNode {
+    float lo[3], hi[3];
+    uint32_t left, right;
+};
+static_assert(sizeof(RNode) == 32, "reference node is 32 B");
+
+// Intersection record: v0, e1 = v1-v0, e2 = v2-v0 (the exact subtractions triIntersect does,
+// modelLoader.h:58-59, so precomputing them is bit-exact), original triangle id.
+struct alignas(16) DTri {
+    float4 a;   // v0.xyz, e1.x
+    float4 b;   // e1.yz, e2.xy
+    float4 c;   // e2.z, id (bits), -, -
+};
+static_assert(sizeof(DTri) == 48, "triangle record is 48 B");
+
+// Shading record by original triangle id: normal + material (modelLoader.h:14-19).
+struct alignas(16) DShade {
+    float nx, ny, nz;
+    int32_t mat;
+};
+
+struct DMat {   // materialDesc (modelLoader.h:21-25)
+    double albedo[3];
+    double emission[3];
+};
+
+// Emissive triangle for the area-CDF pick (kernel.cu:468-495): area precomputed with the
+// reference's float expression length(cross(a1,a2))/2; slot num_lights holds triangle 0,
+// the reference's fallback when nothing is picked.
+struct alignas(16) DLight {
+    float area;
+    int32_t tri;
+    float v0[3], a1[3], a2[3];
+    float pad;
+};
+static_assert(sizeof(DLight) == 48, "light record is 48 B");
+
+struct Cam {    // camera.h:26-34
+    float pos[3];
+    float dist, focal, radius;
+    int32_t w, h;
+};
+
+// ------------------------------------------------------------------ vec3 (vec3.h)
+struct V3 { float x, y, z; };
+__host__ __device__ __forceinline__ V3 v3(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+__host__ __device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ __forceinline__ V3 operator*(V3 a, float f) { return v3(a.x * f, a.y * f, a.z * f); }
+__host__ __device__ __forceinline__ V3 operator/(V3 a, float f) { return v3(a.x / f, a.y / f, a.z / f); }
+__host__ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ V3 cross(V3 a, V3 b)
+{
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__host__ __device__ __forceinline__ float length(V3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__host__ __device__ __forceinline__ V3 normalized(V3 v)
+{
+    float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    return v3(v.x / len, v.y / len, v.z / len);
+}
+
+// ------------------------------------------------------------------ colour (color.h, f64)
+struct C3 { double r, g, b; };
+__device__ __forceinline__ C3 c3(double r, double g, double b) { C3 c; c.r = r; c.g = g; c.b = b; return c; }
+__device__ __forceinline__ C3 cadd(C3 a, C3 b) { return c3(a.r + b.r, a.g + b.g, a.b + b.b); }
+__device__ __forceinline__ C3 cmulf(C3 a, float f) { return c3(a.r * (double)f, a.g * (double)f, a.b * (double)f); }
+__device__ __forceinline__ C3 cdivf(C3 a, float f) { return c3(a.r / (double)f, a.g / (double)f, a.b / (double)f); }
+__device__ __forceinline__ C3 cmul(C3 a, C3 b) { return c3(a.r * b.r, a.g * b.g, a.b * b.b); }
+__device__ __forceinline__ bool czero(C3 a) { return a.r == 0.0 && a.g == 0.0 && a.b == 0.0; }
+
+// ------------------------------------------------------------------ deterministic sin/cos
+// Double-precision Cody-Waite reduction + Taylor polynomials, rounded once to float; plain
+// IEEE double ops in a fixed order, shared with the host (camera) and mirrored by the oracle.
+__host__ __device__ __forceinline__ void det_sincos(float theta, float* s_out, float* c_out)
+{
+    const double x = (double)theta;
+    const double kd = rint(x * 0.6366197723675814);
+    const int k = (int)kd;
+    const double r = (x - kd * 1.5707963267948966) - kd * 6.123233995736766e-17;
+    const double r2 = r * r;
+    double sp = 2.8114572543455206e-15;
+    sp = sp * r2 + -7.647163731819816e-13;
+    sp = sp * r2 + 1.6059043836821613e-10;
+    sp = sp * r2 + -2.505210838544172e-08;
+    sp = sp * r2 + 2.7557319223985893e-06;
+    sp = sp * r2 + -0.0001984126984126984;
+    sp = sp * r2 + 0.008333333333333333;
+    sp = sp * r2 + -0.16666666666666666;
+    const double sn = r + r * (r2 * sp);
+    double cp = -1.5619206968586225e-16;
+    cp = cp * r2 + 4.779477332387385e-14;
+    cp = cp * r2 + -1.1470745597729725e-11;
+    cp = cp * r2 + 2.08767569878681e-09;
+    cp = cp * r2 + -2.755731922398589e-07;
+    cp = cp * r2 + 2.48015873015873e-05;
+    cp = cp * r2 + -0.001388888888888889;
+    cp = cp * r2 + 0.041666666666666664;
+    cp = cp * r2 + -0.5;
+    const double cs = 1.0 + r2 * cp;
+    double sv, cv;
+    switch (k & 3) {
+    case 0: sv = sn; cv = cs; break;
+    case 1: sv = cs; cv = -sn; break;
+    case 2: sv = -sn; cv = -cs; break;
+    default: sv = -cs; cv = sn; break;
+    }
+    *s_out = (float)sv;
+    *c_out = (float)cv;
+}
+
+// ------------------------------------------------------------------ XORWOW (cuRAND)
+struct Rng {
+    uint32_t d, v0, v1, v2, v3, v4;
+};
+
+__device__ __forceinline__ uint32_t rng_next(Rng& s)
+{
+    const uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1; s.v1 = s.v2; s.v2 = s.v3; s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+
+// curand_uniform (kernel.cu:58): x * 2^-32 + 2^-33 in float, contracted as nvcc emits it.
+__device__ __forceinline__ float rng_uniform(Rng& s)
+{
+    return __builtin_fmaf((float)rng_next(s), 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+}
+
+// curand_init(seed, subsequence, 0) (kernel.cu:532): cuRAND seeding salts, then
+// v <- A^(subsequence * 2^67) v through the tables J_k = A^(2^(67+k)) (160 rows x 5 words).
+__device__ __forceinline__ void rng_init(Rng& s, uint64_t seed, uint32_t subseq, const uint32_t* __restrict__ jump)
+{
+    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    s.d = 6615241u + t1 + t0;
+    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    for (int k = 0; k < 32; ++k) {
+        if (!((subseq >> k) & 1u)) continue;
+        const uint32_t* m = jump + (size_t)k * 800;
+        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+#pragma unroll
+        for (int w = 0; w < 5; ++w) {
+            uint32_t bits = v[w];
+            while (bits) {
+                const int b = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t* row = m + (w * 32 + b) * 5;
+                r0 ^= row[0]; r1 ^= row[1]; r2 ^= row[2]; r3 ^= row[3]; r4 ^= row[4];
+            }
+        }
+        v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+    }
+    s.v0 = v[0]; s.v1 = v[1]; s.v2 = v[2]; s.v3 = v[3]; s.v4 = v[4];
+}
+
+// ------------------------------------------------------------------ geometry tests
+// triIntersect (modelLoader.h:49-83) on a precomputed {v0, e1, e2} record.
+__device__ __forceinline__ float tri_t(V3 o, V3 d, V3 v0, V3 e1, V3 e2)
+{
+    const V3 q = cross(d, e2);
+    const float a = dot(e1, q);
+    if ((double)__builtin_fabsf(a) < 0.00001) return kMaxFloat;
+    const V3 s = (o - v0) / a;
+    const V3 r = cross(s, e1);
+    const float b0 = dot(s, q);
+    const float b1 = dot(r, d);
+    const float b2 = 1.0f - b0 - b1;
+    if (b0 < 0.0f) return kMaxFloat;
+    if (b1 < 0.0f) return kMaxFloat;
+    if (b2 < 0.0f) return kMaxFloat;
+    return dot(e2, r);
+}
+
+__device__ __forceinline__ float tri_t_rec(V3 o, V3 d, const DTri* __restrict__ tr, uint32_t* id)
+{
+    const float4 a = tr->a, b = tr->b, c = tr->c;
+    *id = __float_as_uint(c.y);
+    return tri_t(o, d, v3(a.x, a.y, a.z), v3(a.w, b.x, b.y), v3(b.z, b.w, c.x));
+}
+
+// rayAABBIntersect (BVH.h:51-83): IEEE divisions, compare/swap with the reference's NaN
+// behaviour.  Also returns a conservative entry/exit (NaN-ignoring max/min of the slab
+// values) that the culled walk uses for ordering and distance culling only.
+__device__ __forceinline__ bool slab_ref(V3 o, V3 d, float lx, float ly, float lz, float hx, float hy, float hz,
+                                         float* t_in, float* t_out)
+{
+    float tmin = (lx - o.x) / d.x, tmax = (hx - o.x) / d.x, tt;
+    if (tmin > tmax) { tt = tmin; tmin = tmax; tmax = tt; }
+    float tymin = (ly - o.y) / d.y, tymax = (hy - o.y) / d.y;
+    if (tymin > tymax) { tt = tymin; tymin = tymax; tymax = tt; }
+    float tzmin = (lz - o.z) / d.z, tzmax = (hz - o.z) / d.z;
+    if (tzmin > tzmax) { tt = tzmin; tzmin = tzmax; tzmax = tt; }
+    *t_in = __builtin_fmaxf(__builtin_fmaxf(tmin, tymin), tzmin);
+    *t_out = __builtin_fminf(__builtin_fminf(tmax, tymax), tzmax);
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    return true;
+}
+
+// ------------------------------------------------------------------ traversal results
+struct Hit {
+    int32_t tri;     // original triangle id, -1 = miss
+    float t;         // closestT (MAX_FLOAT on miss)
+};
+
+struct Counters {
+    uint32_t nodes, tris;
+};
+
+// kernel.cu:112-161 trace(): the reference's exact walk -- left child first, every box the
+// line overlaps, strict 0 < t < closestT.  The stack lives in LDS (kStack entries per lane,
+// lane-interleaved: entry k of lane l at stack[k*64 + l]).
+template <bool kCount>
+__device__ __forceinline__ Hit trace_reference(V3 o, V3 d, const RNode* __restrict__ nodes, const DTri* __restrict__ tris,
+                                               uint32_t* stack, int lane, Counters& cnt)
+{
+    float closest = kMaxFloat;
+    int32_t best = -1;
+    int i = 0;
+    stack[lane] = 0;
+    while (i >= 0) {
+        const uint32_t e = stack[i * 64 + lane];
+        if (e & kLeaf) {
+            const uint32_t k = e ^ kLeaf;
+            uint32_t id;
+            const float t = tri_t_rec(o, d, tris + k, &id);
+            if (0.0f < t && t < closest) { closest = t; best = (int32_t)k; }
+            if (kCount) ++cnt.tris;
+            --i;
+        } else {
+            const RNode* nd = nodes + e;
+            const float4 p = *reinterpret_cast<const float4*>(nd);
+            const float4 q = *reinterpret_cast<const float4*>(&nd->hi[1]);
+            if (kCount) ++cnt.nodes;
+            float ti, to;
+            // p = lo.xyz, hi.x ; q = hi.yz, left, right
+            if (slab_ref(o, d, p.x, p.y, p.z, p.w, q.x, q.y, &ti, &to)) {
+                stack[i * 64 + lane] = __float_as_uint(q.w);
+                stack[(i + 1) * 64 + lane] = __float_as_uint(q.z);
+                ++i;
+            } else {
+                --i;
+            }
+        }
+    }
+    Hit h;
+    h.tri = best;
+    h.t = closest;
+    return h;
+}
+
+// Distance-culled, near-first walk over the 64-B child-pair records.  It returns the SAME
+// hit as trace_reference: the winner is the minimum of (t, DFS rank) over 0 < t < MAX_FLOAT,
+// which is what the reference's left-first strict '<' scan selects; boxes are entered only if
+// the reference's own slab test accepts them; and a box is skipped only when its entry
+// distance exceeds the current best by the relative margin cull_rel, or its exit lies behind
+// the origin by more than cull_abs (DESIGN.md "Traversal").  Stack entries are (node, entry t).
+template <bool kCount>
+__device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const DNode* __restrict__ nodes,
+                                            const DTri* __restrict__ tris, uint32_t* stack, int lane,
+                                            float cull_rel, float cull_abs, Counters& cnt)
+{
+    // best_slot starts at 0 so a tie with the MAX_FLOAT sentinel is never accepted (the
+    // reference needs t < closestT = MAX_FLOAT); best_id = ~0 marks "no hit yet".
+    float best_t = kMaxFloat;
+    uint32_t best_slot = 0u;
+    uint32_t best_id = 0xffffffffu;
+    float ti, to;
+    if (kCount) ++cnt.nodes;
+    if (!slab_ref(o, d, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) || to < -cull_abs) {
+        Hit h; h.tri = -1; h.t = kMaxFloat; return h;
+    }
+    int sp = 0;
+    uint32_t node = 0;
+    for (;;) {
+        const DNode* nd = nodes + node;
+        const float4 A = nd->a, B = nd->b, C = nd->c;
+        const uint4 D = nd->d;
+        bool h0 = false, h1 = false;
+        float t0 = 0.0f, t1 = 0.0f;
+        if (D.x & kLeaf) {
+            const uint32_t slot = D.x ^ kLeaf;
+            uint32_t id;
+            const float t = tri_t_rec(o, d, tris + slot, &id);
+            if (kCount) ++cnt.tris;
+            if (0.0f < t && (t < best_t || (t == best_t && slot < best_slot))) { best_t = t; best_slot = slot; best_id = id; }
+        } else {
+            const bool hit = slab_ref(o, d, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to);
+            if (kCount) ++cnt.nodes;
+            h0 = hit && !(to < -cull_abs) && !(ti > best_t * cull_rel);
+            t0 = ti;
+        }
+        if (D.y & kLeaf) {
+            const uint32_t slot = D.y ^ kLeaf;
+            uint32_t id;
+            const float t = tri_t_rec(o, d, tris + slot, &id);
+            if (kCount) ++cnt.tris;
+            if (0.0f < t && (t < best_t || (t == best_t && slot < best_slot))) { best_t = t; best_slot = slot; best_id = id; }
+            // a leaf found now may already beat the left box: re-check it
+            h0 = h0 && !(t0 > best_t * cull_rel);
+        } else {
+            const bool hit = slab_ref(o, d, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to);
+            if (kCount) ++cnt.nodes;
+            h1 = hit && !(to < -cull_abs) && !(ti > best_t * cull_rel);
+            t1 = ti;
+        }
+        if (h0 && h1) {
+            const bool swap = t1 < t0;
+            const uint32_t nearn = swap ? D.y : D.x;
+            const uint32_t farn = swap ? D.x : D.y;
+            const float fart = swap ? t0 : t1;
+            stack[sp * 128 + lane] = farn;
+            stack[sp * 128 + 64 + lane] = __float_as_uint(fart);
+            ++sp;
+            node = nearn;
+            continue;
+        }
+        if (h0) { node = D.x; continue; }
+        if (h1) { node = D.y; continue; }
+        // pop, skipping entries the current best already beats
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            const float et = __uint_as_float(stack[sp * 128 + 64 + lane]);
+            if (et > best_t * cull_rel) continue;
+            node = stack[sp * 128 + lane];
+            found = true;
+            break;
+        }
+        if (!found) break;
+    }
+    Hit h;
+    h.tri = (best_id == 0xffffffffu) ? -1 : (int32_t)best_id;
+    h.t = best_t;
+    return h;
+}
+
+}  // namespace ptd

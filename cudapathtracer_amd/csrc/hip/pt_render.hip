@@ -1,0 +1,791 @@
+// pt_render.hip -- gfx950 render kernels and the render half of the C-ABI (include/pt/pt.h).
+//
+// One wave renders one 8x8 image tile: lane l owns pixel (8*tx + mx(l), 8*ty + my(l)) with
+// (mx, my) the Morton decode of l, and runs ALL of that pixel's samples in order with its
+// XORWOW state and f64 running mean in registers (the reference keeps both in HBM and
+// re-launches drawPixel per sample, kernel.cu:535-553, 709-736).  Waves are persistent and pull
+// tiles from an atomic counter; tile t belongs to shard t % shard_count.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../host/host_internal.h"
+#include "pt_device.h"
+
+using namespace ptd;
+
+namespace {
+
+constexpr uint32_t kTile = 8;   // 8x8 = 64 pixels = one wave
+
+struct Args {
+    const DNode* nodes;
+    const RNode* rnodes;
+    const DTri* tris_leaf;     // DFS leaf order (culled walk)
+    const DTri* tris_orig;     // original order (reference walk)
+    const DShade* shade;
+    const DMat* mats;
+    const DLight* lights;
+    const uint32_t* jump;
+    float* out;
+    unsigned long long* counters;   // [0] traced [1] reference [2] nodes [3] tris [4] samples
+    uint32_t* tile_counter;
+    uint32_t num_lights;
+    float total_light_area;
+    float root[6];
+    Cam cam;
+    int32_t w, h, spp, bounces;
+    uint32_t flags;
+    uint64_t seed;
+    int32_t shard_index, shard_count;
+    uint32_t tiles_x, ntiles_shard;
+    uint32_t stack_words;           // LDS words per wave
+    float cull_rel, cull_abs;
+};
+
+// ------------------------------------------------------------------ per-lane tracer
+template <bool kRefWalk, bool kCount>
+struct Tracer {
+    const Args* a;
+    uint32_t* stack;
+    int lane;
+    Counters cnt;
+    uint32_t traced;
+    uint32_t reference;
+    // primary-ray memo (exact: keyed on the ray's bits)
+    bool have;
+    uint32_t ko[3], kd[3];
+    Hit kh;
+
+    __device__ Hit trace(V3 o, V3 d)
+    {
+        ++traced;
+        if (kRefWalk)
+            return trace_reference<kCount>(o, d, a->rnodes, a->tris_orig, stack, lane, cnt);
+        return trace_culled<kCount>(o, d, a->root, a->nodes, a->tris_leaf, stack, lane, a->cull_rel, a->cull_abs, cnt);
+    }
+
+    __device__ Hit trace_primary(V3 o, V3 d, bool memo)
+    {
+        ++reference;
+        if (memo && have && ko[0] == __float_as_uint(o.x) && ko[1] == __float_as_uint(o.y) &&
+            ko[2] == __float_as_uint(o.z) && kd[0] == __float_as_uint(d.x) && kd[1] == __float_as_uint(d.y) &&
+            kd[2] == __float_as_uint(d.z))
+            return kh;
+        Hit h = trace(o, d);
+        if (memo) {
+            have = true;
+            ko[0] = __float_as_uint(o.x); ko[1] = __float_as_uint(o.y); ko[2] = __float_as_uint(o.z);
+            kd[0] = __float_as_uint(d.x); kd[1] = __float_as_uint(d.y); kd[2] = __float_as_uint(d.z);
+            kh = h;
+        }
+        return h;
+    }
+
+    __device__ Hit trace_secondary(V3 o, V3 d)
+    {
+        ++reference;
+        return trace(o, d);
+    }
+};
+
+__device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
+{
+    const float4 q = *reinterpret_cast<const float4*>(s + tri);
+    return v3(q.x, q.y, q.z);
+}
+__device__ __forceinline__ int32_t ld_mat(const DShade* s, int32_t tri) { return s[tri].mat; }
+
+// kernel.cu:44-54
+__device__ __forceinline__ V3 get_tangent(V3 n)
+{
+    const V3 c1 = cross(n, v3(0, 0, 1));
+    const V3 c2 = cross(n, v3(0, 1, 0));
+    return (dot(c1, c1) > dot(c2, c2)) ? c1 : c2;
+}
+__device__ __forceinline__ V3 to_frame(V3 n, float lx, float ly, float lz)   // kernel.cu:70-75, 91-96
+{
+    const V3 tg = get_tangent(n);
+    const V3 bt = cross(n, tg);
+    return normalized(n * ly + tg * lx + bt * lz);
+}
+__device__ __forceinline__ V3 cosine_ray(V3 n, Rng& rng)                     // kernel.cu:78-99
+{
+    const float u1 = rng_uniform(rng);
+    const float u2 = rng_uniform(rng);
+    const float r = sqrtf(u1);
+    const float theta = (float)(2 * 3.14159 * (double)u2);
+    float s, c;
+    det_sincos(theta, &s, &c);
+    const float x = r * c;
+    const float z = r * s;
+    const float y = sqrtf(__builtin_fmaxf(0.0f, 1.0f - u1));
+    return to_frame(n, x, y, z);
+}
+__device__ __forceinline__ V3 rand_ray(V3 n, Rng& rng)                       // kernel.cu:60-77
+{
+    const float u1 = rng_uniform(rng);
+    const float u2 = rng_uniform(rng);
+    const float r = sqrtf(1.0f - u1 * u1);
+    const float phi = (float)(2 * 3.14159 * (double)u2);
+    float s, c;
+    det_sincos(phi, &s, &c);
+    return to_frame(n, r * c, u1, r * s);
+}
+__device__ __forceinline__ C3 mat_albedo(const DMat* m) { return c3(m->albedo[0], m->albedo[1], m->albedo[2]); }
+__device__ __forceinline__ C3 mat_emission(const DMat* m) { return c3(m->emission[0], m->emission[1], m->emission[2]); }
+__device__ __forceinline__ C3 brdf(const DMat* m) { return cmulf(mat_albedo(m), (float)(1 / 3.14159)); }  // kernel.cu:101-104
+
+// Area-CDF pick over the emissive triangles + uniform point (kernel.cu:466-495 / 231-262).
+// The scan stops once randArea <= 0: no later light can then satisfy randArea > 0 (areas are
+// >= 0), so the selection is unchanged.
+__device__ __forceinline__ int32_t pick_light(const Args& a, Rng& rng, V3* p)
+{
+    float ra = a.total_light_area * rng_uniform(rng);
+    uint32_t sel = a.num_lights;   // slot of triangle 0 (nothing picked)
+    for (uint32_t j = 0; j < a.num_lights && ra > 0; ++j) {
+        const float area = a.lights[j].area;
+        if (ra < area && ra > 0) sel = j;
+        ra -= area;
+    }
+    float u = rng_uniform(rng);
+    float v = rng_uniform(rng);
+    const DLight& L = a.lights[sel];
+    const V3 v0 = v3(L.v0[0], L.v0[1], L.v0[2]);
+    const V3 a1 = v3(L.a1[0], L.a1[1], L.a1[2]);
+    const V3 a2 = v3(L.a2[0], L.a2[1], L.a2[2]);
+    if ((double)(u + v) > 1.0) {
+        u = (float)((double)u + 2 * (0.5 - (double)u));
+        v = (float)((double)v + 2 * (0.5 - (double)v));
+    }
+    *p = v0 + a1 * u + a2 * v;
+    return L.tri;
+}
+
+// ------------------------------------------------------------------ integrator 0
+// radianceAlongSingleStep2, kernel.cu:417-515.  Dead-path skip: once weight == 0 every later
+// bounce adds weight*Le = 0, so (unless PT_FLAG_NO_DEAD_PATH_SKIP) the lane stops tracing and
+// only replays the RNG draws each remaining bounce would make (1 + 2, or 1 + 3 and the
+// i = max(i, D-2) jump), keeping its stream aligned with the reference.
+template <bool kRefWalk, bool kCount>
+__device__ C3 radiance_unidir(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 o, V3 dir, Rng& rng, bool skip_dead,
+                              bool memo)
+{
+    C3 accum = c3(0, 0, 0);
+    C3 weight = c3(1, 1, 1);
+    const int D = a.bounces;
+    for (int i = 0; i < D; ++i) {
+        if (skip_dead && i > 0 && czero(weight)) {
+            ++tr.reference;
+            const float u = rng_uniform(rng);
+            if (u < 0.5) { rng_next(rng); rng_next(rng); }
+            else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
+            continue;
+        }
+        Hit h = (i == 0) ? tr.trace_primary(o, dir, memo) : tr.trace_secondary(o, dir);
+        int32_t tri = h.tri;
+        float t = (float)((double)h.t - 0.001);                                 // :431
+        if ((double)t < 0.001) weight = c3(0, 0, 0);                             // :432
+        if (t > kMaxFloat - 1) { weight = c3(0, 0, 0); tri = 0; t = 0; }         // :436
+        const int32_t mi = ld_mat(a.shade, tri);
+        const DMat* cm = a.mats + mi;
+        const V3 normal = ld_norm(a.shade, tri);
+        const V3 pos = o + dir * t;                                               // :449
+        if (cm->emission[0] != 0) {                                               // :453
+            accum = cadd(accum, cmul(weight, mat_emission(cm)));
+            weight = c3(0, 0, 0);
+        }
+        V3 ldir;
+        const float u = rng_uniform(rng);
+        if (u < 0.5) {                                                            // :460
+            ldir = cosine_ray(normal, rng);
+            weight = cmul(weight, cmulf(brdf(cm), (float)3.14159));
+        } else {                                                                  // :466
+            V3 p1;
+            pick_light(a, rng, &p1);
+            const V3 d = p1 - pos;
+            ldir = normalized(d);
+            const float inv_prob = a.total_light_area;
+            const float cos_l = __builtin_fmaxf(0.0f, dot(ldir, normal));
+            const float cos_o = __builtin_fmaxf(0.0f, dot(v3(0, -1, 0), ldir * -1));
+            const float G = cos_l * cos_o / dot(d, d);
+            weight = cmul(weight, cmulf(cmulf(brdf(cm), G), inv_prob));
+            i = (i > D - 2) ? i : D - 2;
+        }
+        o = pos;
+        dir = ldir;
+    }
+    return accum;
+}
+
+// ------------------------------------------------------------------ integrator 1
+__device__ __forceinline__ float geo_term(V3 xa, V3 xb, V3 na, V3 nb)      // kernel.cu:370-373
+{
+    const V3 seg = xa - xb;
+    const V3 ray = normalized(seg);
+    float G = __builtin_fabsf(dot(ray, na) * dot(ray, nb)) / dot(seg, seg);
+    if (G != G) G = 0;
+    return G;
+}
+
+// radianceAlongSingleStep, kernel.cu:217-415 (decision d2: a miss on the camera's second
+// bounce uses triangle 0 and t = 0 instead of reading tris[-1]).
+template <bool kRefWalk, bool kCount>
+__device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_o, V3 cam_d, Rng& rng, bool memo)
+{
+    V3 x[5], nrm[5];
+    int32_t mat[5] = {0, 0, 0, 0, 0};
+    float ip[5];
+    {
+        V3 p;
+        const int32_t sel = pick_light(a, rng, &p);
+        const V3 n = ld_norm(a.shade, sel);
+        x[0] = p + n * 0.001f;
+        nrm[0] = n;
+        mat[0] = ld_mat(a.shade, sel);
+        ip[0] = a.total_light_area;
+    }
+    {
+        const V3 od = rand_ray(nrm[0], rng);
+        Hit h = tr.trace_secondary(x[0], od);
+        int32_t tri = h.tri;
+        float t = (float)((double)h.t - 0.001);
+        if (t > kMaxFloat - 1) { tri = 0; t = 0; }
+        const V3 n2 = ld_norm(a.shade, tri);
+        const V3 pos = x[0] + od * t;
+        const float G = __builtin_fabsf(dot(n2, od)) / __builtin_fmaxf(0.001f, t * t);
+        x[1] = pos; nrm[1] = n2; mat[1] = ld_mat(a.shade, tri);
+        ip[1] = (float)(2 * 3.14159 / (double)G);
+    }
+    x[4] = cam_o; nrm[4] = cam_d; ip[4] = 1;
+    {
+        Hit h = tr.trace_primary(cam_o, cam_d, memo);
+        int32_t tri = h.tri;
+        float t = (float)((double)h.t - 0.001);
+        if (t > kMaxFloat - 1) { tri = 0; t = 0; }
+        x[3] = cam_o + cam_d * t;
+        nrm[3] = ld_norm(a.shade, tri);
+        mat[3] = ld_mat(a.shade, tri);
+        ip[3] = 1;
+    }
+    {
+        const V3 d = cosine_ray(nrm[3], rng);
+        Hit h = tr.trace_secondary(x[3], d);
+        int32_t tri = h.tri;
+        float t = (float)((double)h.t - 0.001);
+        if (t > kMaxFloat - 1 || tri < 0) { tri = 0; t = 0; }
+        const V3 n = ld_norm(a.shade, tri);
+        float G = __builtin_fabsf(dot(nrm[3], d) * dot(n, d)) / (t * t);
+        if (G == 0) G = 1;
+        if (G != G) G = 1;
+        x[2] = x[3] + d * t;
+        nrm[2] = n;
+        mat[2] = ld_mat(a.shade, tri);
+        ip[2] = (float)(3.14159 / (double)G);
+    }
+    C3 accum = c3(0, 0, 0);
+    const C3 le = mat_emission(a.mats + mat[0]);
+    const C3 e3 = mat_emission(a.mats + mat[3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 2; j < 4; ++j) {
+            C3 w = cmulf(le, ip[0]);
+#pragma unroll
+            for (int k = 1; k <= i; ++k) {
+                const float G = geo_term(x[k], x[k - 1], nrm[k], nrm[k - 1]);
+                w = cmulf(cmulf(cmul(w, cdivf(mat_albedo(a.mats + mat[k]), 3.14159f)), G), ip[k]);
+            }
+#pragma unroll
+            for (int k = j + 1; k < 4; ++k) {
+                const float G = geo_term(x[k], x[k - 1], nrm[k], nrm[k - 1]);
+                w = cmulf(cmulf(cmul(w, cdivf(mat_albedo(a.mats + mat[k]), 3.14159f)), G), ip[k]);
+            }
+            const V3 seg = x[j] - x[i];
+            const float len = length(seg);
+            const V3 ray = normalized(seg);
+            float G = __builtin_fmaxf(0.0f, dot(ray, nrm[j]) * dot(ray * -1, nrm[i])) / dot(seg, seg);
+            if (G != G) G = 0;
+            w = cmulf(cmulf(cmul(w, cdivf(mat_albedo(a.mats + mat[j]), 3.14159f)), G), ip[j]);
+            const float m = (float)fmax(w.r, fmax(w.g, w.b));
+            float V = 0;
+            if ((double)m > 0.01) {
+                Hit h = tr.trace_secondary(x[i], ray);
+                if ((double)__builtin_fabsf(h.t - len) <= 0.01) V = 1;
+            }
+            w = cmulf(w, V);
+            accum = cadd(accum, w);
+            accum = cadd(accum, e3);
+        }
+    }
+    return accum;
+}
+
+// ------------------------------------------------------------------ camera (camera.h:77-97)
+__device__ __forceinline__ void camera_ray(const Cam& cam, uint32_t px, uint32_t py, bool lens, float u1, float u2,
+                                           V3* o, V3* d)
+{
+    V3 film = v3((float)px / (float)cam.w - 0.5f, (float)py / (float)cam.h - 0.5f, 0.0f);
+    V3 lo = v3(0.0f, 0.0f, 0.0f);
+    if (lens) {
+        const float r = cam.radius * sqrtf(u1);
+        const float theta = (float)(2 * 3.14159 * (double)u2);
+        float s, c;
+        det_sincos(theta, &s, &c);
+        lo = v3(r * c, r * s, 0.0f);
+    }
+    film.z = cam.dist;
+    film = (film * -cam.focal) / cam.dist;
+    *o = lo + v3(cam.pos[0], cam.pos[1], cam.pos[2]);
+    *d = normalized(film - lo);
+}
+
+__device__ __forceinline__ uint32_t morton2(uint32_t x, uint32_t y)   // camera.h:66-75
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        r |= ((x >> b) & 1u) << (2 * b);
+        r |= ((y >> b) & 1u) << (2 * b + 1);
+    }
+    return r;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ the render kernel
+template <int kIntegrator, bool kRefWalk, bool kCount>
+__global__ __launch_bounds__(64) void render_tiles(Args a)
+{
+    extern __shared__ uint32_t lds_stack[];
+    const int lane = threadIdx.x;
+    Tracer<kRefWalk, kCount> tr;
+    tr.a = &a;
+    tr.stack = lds_stack;
+    tr.lane = lane;
+    tr.cnt.nodes = 0;
+    tr.cnt.tris = 0;
+    tr.traced = 0;
+    tr.reference = 0;
+    unsigned long long samples = 0;
+    const bool skip_dead = !(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP);
+    const bool memo = !(a.flags & PT_FLAG_NO_PRIMARY_CACHE);
+    const uint32_t mx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4);
+    const uint32_t my = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(a.tile_counter, 1u);
+        k = __shfl(k, 0, 64);
+        if (k >= a.ntiles_shard) break;
+        const uint32_t t = (uint32_t)a.shard_index + k * (uint32_t)a.shard_count;
+        const uint32_t px = (t % a.tiles_x) * kTile + mx;
+        const uint32_t py = (t / a.tiles_x) * kTile + my;
+        if (px >= (uint32_t)a.w || py >= (uint32_t)a.h) continue;
+        const uint32_t idx = morton2(px, py);
+        Rng rng;
+        rng_init(rng, a.seed, idx, a.jump);
+        const bool lens = (idx == 0) || (a.cam.radius != 0.0f);
+        tr.have = false;
+        double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+        for (int n = 1; n <= a.spp; ++n) {
+            float u1 = 0.0f, u2 = 0.0f;
+            if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
+            V3 o, d;
+            camera_ray(a.cam, px, py, lens, u1, u2, &o, &d);
+            C3 L;
+            if (kIntegrator == PT_INTEGRATOR_HEAD) L = radiance_head(a, tr, o, d, rng, memo);
+            else L = radiance_unidir(a, tr, o, d, rng, skip_dead, memo);
+            const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
+            m0 = (m0 * fn1) / fn + L.r / fn;
+            m1 = (m1 * fn1) / fn + L.g / fn;
+            m2 = (m2 * fn1) / fn + L.b / fn;
+        }
+        samples += (unsigned long long)a.spp;
+        float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+        o3[0] = (float)m0;
+        o3[1] = (float)m1;
+        o3[2] = (float)m2;
+    }
+    const unsigned long long c0 = wave_sum(tr.traced), c1 = wave_sum(tr.reference), c4 = wave_sum(samples);
+    unsigned long long c2 = 0, c3v = 0;
+    if (kCount) { c2 = wave_sum(tr.cnt.nodes); c3v = wave_sum(tr.cnt.tris); }
+    if (lane == 0) {
+        atomicAdd(a.counters + 0, c0);
+        atomicAdd(a.counters + 1, c1);
+        atomicAdd(a.counters + 4, c4);
+        if (kCount) { atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) return pt::fail(PT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src)
+{
+    size_t bytes = src.size() * sizeof(T);
+    if (bytes == 0) bytes = sizeof(T);
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), bytes));
+    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+}  // namespace
+
+// GF(2) jump tables J_k = A^(2^(67+k)), k = 0..31, rocRAND's bit-image layout.
+static void build_jump_tables(std::vector<uint32_t>& out)
+{
+    auto apply = [](const uint32_t* img, uint32_t v[5]) {
+        uint32_t r[5] = {0, 0, 0, 0, 0};
+        for (int b = 0; b < 160; ++b)
+            if ((v[b >> 5] >> (b & 31)) & 1u)
+                for (int w = 0; w < 5; ++w) r[w] ^= img[b * 5 + w];
+        memcpy(v, r, sizeof(r));
+    };
+    std::vector<uint32_t> m(800), tmp(800);
+    for (int b = 0; b < 160; ++b) {   // one XORWOW step on the 160-bit xorshift state
+        uint32_t v[5] = {0, 0, 0, 0, 0};
+        v[b >> 5] = 1u << (b & 31);
+        const uint32_t t = v[0] ^ (v[0] >> 2);
+        uint32_t nv[5] = {v[1], v[2], v[3], v[4], (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1))};
+        memcpy(&m[b * 5], nv, sizeof(nv));
+    }
+    auto square = [&]() {
+        for (int b = 0; b < 160; ++b) {
+            uint32_t v[5];
+            memcpy(v, &m[b * 5], sizeof(v));
+            apply(m.data(), v);
+            memcpy(&tmp[b * 5], v, sizeof(v));
+        }
+        m.swap(tmp);
+    };
+    for (int i = 0; i < 67; ++i) square();
+    out.resize(32 * 800);
+    for (int k = 0; k < 32; ++k) {
+        memcpy(&out[k * 800], m.data(), 800 * sizeof(uint32_t));
+        square();
+    }
+}
+
+void pt::sincos_det(float theta, float* s, float* c) { det_sincos(theta, s, c); }
+
+struct pt_ctx {
+    int device = 0;
+    DNode* nodes = nullptr;
+    RNode* rnodes = nullptr;
+    DTri* tris_leaf = nullptr;
+    DTri* tris_orig = nullptr;
+    DShade* shade = nullptr;
+    DMat* mats = nullptr;
+    DLight* lights = nullptr;
+    uint32_t* jump = nullptr;
+    unsigned long long* counters = nullptr;
+    uint32_t* tile_counter = nullptr;
+    float* scratch_out = nullptr;
+    size_t scratch_bytes = 0;
+    uint32_t num_lights = 0;
+    float total_light_area = 0;
+    float root[6];
+    int32_t depth = 0;
+    uint32_t num_tris = 0;
+    float scene_extent = 1.0f;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int num_cus = 256;
+};
+
+extern "C" {
+
+pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
+{
+    auto bail = [&](int code) -> pt_ctx* { if (err) *err = code; return nullptr; };
+    if (!sc || !sc->verts || !sc->tris || !sc->mats || !sc->bvh) return bail(pt::fail(PT_E_INVALID, "pt_create: incomplete scene"));
+    if (sc->num_tris < 2 || sc->bvh_size != sc->num_tris - 1)
+        return bail(pt::fail(PT_E_SCENE, "pt_create: need >= 2 triangles and a BVH of num_tris-1 nodes (got %u tris, %u nodes)",
+                             sc->num_tris, sc->bvh_size));
+    if (sc->bvh_depth >= PT_MAX_BVH_DEPTH)
+        return bail(pt::fail(PT_E_BVH_DEPTH, "Critical Error: BVH depth is too big (%d)", sc->bvh_depth));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return bail(pt::fail(PT_E_NODEV, "pt_create: no HIP device"));
+    if (device < 0 || device >= ndev) return bail(pt::fail(PT_E_NODEV, "pt_create: device %d out of range (%d)", device, ndev));
+    if (hipSetDevice(device) != hipSuccess) return bail(pt::fail(PT_E_HIP, "hipSetDevice(%d) failed", device));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(pt::fail(PT_E_HIP, "hipGetDeviceProperties failed"));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return bail(pt::fail(PT_E_NODEV, "pt_create: device %d is %s, this build targets gfx950", device, prop.gcnArchName));
+
+    const uint32_t nt = sc->num_tris, nn = sc->bvh_size;
+    for (uint32_t i = 0; i < nt; ++i) {
+        const pt_triangle& t = sc->tris[i];
+        if ((uint32_t)t.v0 >= sc->num_verts || (uint32_t)t.v1 >= sc->num_verts || (uint32_t)t.v2 >= sc->num_verts ||
+            (uint32_t)t.mat >= sc->num_mats)
+            return bail(pt::fail(PT_E_SCENE, "pt_create: triangle %u has an out-of-range vertex or material index", i));
+    }
+    for (uint32_t j = 0; j < sc->num_lights; ++j)
+        if (sc->lights[j] >= nt) return bail(pt::fail(PT_E_SCENE, "pt_create: light %u indexes triangle %u", j, sc->lights[j]));
+    // validate the BVH: every reference must be in range, every triangle reachable once
+    std::vector<uint32_t> leaf_rank(nt, 0xffffffffu);
+    std::vector<uint32_t> leaf_order;
+    leaf_order.reserve(nt);
+    {
+        std::vector<uint32_t> st;
+        st.push_back(0);
+        size_t visits = 0;
+        while (!st.empty()) {   // left-first DFS = the order trace() meets leaves
+            const uint32_t e = st.back();
+            st.pop_back();
+            if (++visits > 4ull * nt + 8) return bail(pt::fail(PT_E_SCENE, "pt_create: BVH is not a tree"));
+            if (e & PT_BVH_LEAF_FLAG) {
+                const uint32_t k = e ^ PT_BVH_LEAF_FLAG;
+                if (k >= nt || leaf_rank[k] != 0xffffffffu) return bail(pt::fail(PT_E_SCENE, "pt_create: bad BVH leaf %u", k));
+                leaf_rank[k] = (uint32_t)leaf_order.size();
+                leaf_order.push_back(k);
+            } else {
+                if (e >= nn) return bail(pt::fail(PT_E_SCENE, "pt_create: BVH child %u out of range", e));
+                st.push_back(sc->bvh[e].right);
+                st.push_back(sc->bvh[e].left);
+            }
+        }
+        if (leaf_order.size() != nt) return bail(pt::fail(PT_E_SCENE, "pt_create: BVH reaches %zu of %u triangles", leaf_order.size(), nt));
+    }
+
+    pt_ctx* c = new (std::nothrow) pt_ctx();
+    if (!c) return bail(pt::fail(PT_E_OOM, "pt_create: out of host memory"));
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    c->num_tris = nt;
+    c->depth = sc->bvh_depth;
+
+    auto tri_rec = [&](uint32_t k) {
+        const pt_triangle& t = sc->tris[k];
+        const pt_vec3 a = sc->verts[t.v0], b = sc->verts[t.v1], cc = sc->verts[t.v2];
+        DTri r;
+        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;   // modelLoader.h:58
+        const float e2x = cc.x - a.x, e2y = cc.y - a.y, e2z = cc.z - a.z; // modelLoader.h:59
+        r.a = make_float4(a.x, a.y, a.z, e1x);
+        r.b = make_float4(e1y, e1z, e2x, e2y);
+        uint32_t id = k;
+        float idf;
+        memcpy(&idf, &id, 4);
+        r.c = make_float4(e2z, idf, 0.0f, 0.0f);
+        return r;
+    };
+    std::vector<DTri> tl(nt), to(nt);
+    for (uint32_t i = 0; i < nt; ++i) { to[i] = tri_rec(i); tl[i] = tri_rec(leaf_order[i]); }
+    std::vector<RNode> rn(nn);
+    std::vector<DNode> dn(nn);
+    auto box_of = [&](uint32_t ref, float* b) {   // box of a child; leaves carry no box
+        if (ref & PT_BVH_LEAF_FLAG) { for (int q = 0; q < 6; ++q) b[q] = 0.0f; return; }
+        const pt_bvh_node& x = sc->bvh[ref];
+        b[0] = x.lo.x; b[1] = x.lo.y; b[2] = x.lo.z; b[3] = x.hi.x; b[4] = x.hi.y; b[5] = x.hi.z;
+    };
+    auto remap = [&](uint32_t ref) {
+        return (ref & PT_BVH_LEAF_FLAG) ? (PT_BVH_LEAF_FLAG | leaf_rank[ref ^ PT_BVH_LEAF_FLAG]) : ref;
+    };
+    float lo_all[3] = {1e30f, 1e30f, 1e30f}, hi_all[3] = {-1e30f, -1e30f, -1e30f};
+    for (uint32_t i = 0; i < nn; ++i) {
+        const pt_bvh_node& x = sc->bvh[i];
+        memcpy(rn[i].lo, &x.lo, 12);
+        memcpy(rn[i].hi, &x.hi, 12);
+        rn[i].left = x.left;
+        rn[i].right = x.right;
+        float b0[6], b1[6];
+        box_of(x.left, b0);
+        box_of(x.right, b1);
+        dn[i].a = make_float4(b0[0], b0[1], b0[2], b0[3]);
+        dn[i].b = make_float4(b0[4], b0[5], b1[0], b1[1]);
+        dn[i].c = make_float4(b1[2], b1[3], b1[4], b1[5]);
+        dn[i].d = make_uint4(remap(x.left), remap(x.right), 0u, 0u);
+    }
+    {
+        const pt_bvh_node& r = sc->bvh[0];
+        c->root[0] = r.lo.x; c->root[1] = r.lo.y; c->root[2] = r.lo.z;
+        c->root[3] = r.hi.x; c->root[4] = r.hi.y; c->root[5] = r.hi.z;
+        for (int q = 0; q < 3; ++q) { lo_all[q] = c->root[q]; hi_all[q] = c->root[3 + q]; }
+    }
+    {
+        float ext = 0.0f;
+        for (int q = 0; q < 3; ++q) {
+            const float e = std::fabs(hi_all[q]) > std::fabs(lo_all[q]) ? std::fabs(hi_all[q]) : std::fabs(lo_all[q]);
+            ext = ext > e ? ext : e;
+        }
+        c->scene_extent = (ext > 0.0f && std::isfinite(ext)) ? ext : 1.0f;
+    }
+    std::vector<DShade> sh(nt);
+    for (uint32_t i = 0; i < nt; ++i) {
+        sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
+        sh[i].mat = sc->tris[i].mat;
+    }
+    std::vector<DMat> mt(sc->num_mats);
+    for (uint32_t i = 0; i < sc->num_mats; ++i) {
+        for (int q = 0; q < 3; ++q) { mt[i].albedo[q] = sc->mats[i].albedo[q]; mt[i].emission[q] = sc->mats[i].emission[q]; }
+    }
+    std::vector<DLight> lt(sc->num_lights + 1);
+    auto light_rec = [&](uint32_t tri) {
+        const pt_triangle& t = sc->tris[tri];
+        const pt_vec3 a = sc->verts[t.v0], b = sc->verts[t.v1], cc = sc->verts[t.v2];
+        DLight L;
+        const float a1x = b.x - a.x, a1y = b.y - a.y, a1z = b.z - a.z;
+        const float a2x = cc.x - a.x, a2y = cc.y - a.y, a2z = cc.z - a.z;
+        // length(cross(a1, a2)) / 2, kernel.cu:477-478
+        const float cx = a1y * a2z - a1z * a2y, cy = a1z * a2x - a1x * a2z, cz = a1x * a2y - a1y * a2x;
+        L.area = sqrtf(cx * cx + cy * cy + cz * cz) / 2;
+        L.tri = (int32_t)tri;
+        L.v0[0] = a.x; L.v0[1] = a.y; L.v0[2] = a.z;
+        L.a1[0] = a1x; L.a1[1] = a1y; L.a1[2] = a1z;
+        L.a2[0] = a2x; L.a2[1] = a2y; L.a2[2] = a2z;
+        L.pad = 0.0f;
+        return L;
+    };
+    for (uint32_t j = 0; j < sc->num_lights; ++j) lt[j] = light_rec(sc->lights[j]);
+    lt[sc->num_lights] = light_rec(0);
+    c->num_lights = sc->num_lights;
+    c->total_light_area = sc->total_light_area;
+    std::vector<uint32_t> jump;
+    build_jump_tables(jump);
+
+    int rc = PT_OK;
+    if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
+        (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
+        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump))) {
+        pt_destroy(c);
+        return bail(rc);
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        pt_destroy(c);
+        return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
+    }
+    if (err) *err = PT_OK;
+    return c;
+}
+
+void pt_destroy(pt_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
+                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+}
+
+int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* d_out, void* stream_v, pt_stats* st)
+{
+    if (!c || !p || !cam || !d_out) return pt::fail(PT_E_INVALID, "pt_render: null argument");
+    if (p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 65535)
+        return pt::fail(PT_E_INVALID, "pt_render: image size %dx%d out of range (1..65535)", p->width, p->height);
+    if (p->spp < 0) return pt::fail(PT_E_INVALID, "pt_render: spp < 0");
+    if (p->integrator != PT_INTEGRATOR_UNIDIR && p->integrator != PT_INTEGRATOR_HEAD)
+        return pt::fail(PT_E_INVALID, "pt_render: unknown integrator %d", p->integrator);
+    if (p->integrator == PT_INTEGRATOR_UNIDIR && (p->bounces < 1 || p->bounces > 64))
+        return pt::fail(PT_E_INVALID, "pt_render: bounces %d out of range (1..64)", p->bounces);
+    if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
+        return pt::fail(PT_E_INVALID, "pt_render: shard %d of %d", p->shard_index, p->shard_count);
+    if (cam->pxl_width <= 0 || cam->pxl_height <= 0) return pt::fail(PT_E_INVALID, "pt_render: camera pixel size must be > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+
+    Args a;
+    memset(&a, 0, sizeof(a));
+    a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
+    a.shade = c->shade; a.mats = c->mats; a.lights = c->lights; a.jump = c->jump;
+    a.out = d_out; a.counters = c->counters; a.tile_counter = c->tile_counter;
+    a.num_lights = c->num_lights; a.total_light_area = c->total_light_area;
+    memcpy(a.root, c->root, sizeof(a.root));
+    a.cam.pos[0] = cam->pos.x; a.cam.pos[1] = cam->pos.y; a.cam.pos[2] = cam->pos.z;
+    a.cam.dist = cam->dist_from_film; a.cam.focal = cam->focal_length; a.cam.radius = cam->radius;
+    a.cam.w = cam->pxl_width; a.cam.h = cam->pxl_height;
+    a.w = p->width; a.h = p->height; a.spp = p->spp; a.bounces = p->bounces; a.flags = p->flags; a.seed = p->seed;
+    a.shard_index = p->shard_index; a.shard_count = p->shard_count;
+    const uint32_t tx = (p->width + kTile - 1) / kTile, ty = (p->height + kTile - 1) / kTile;
+    const uint32_t ntiles = tx * ty;
+    a.tiles_x = tx;
+    a.ntiles_shard = (ntiles > (uint32_t)p->shard_index) ? (ntiles - (uint32_t)p->shard_index + (uint32_t)p->shard_count - 1) / (uint32_t)p->shard_count : 0;
+    a.cull_rel = 1.0f + 1.0f / 1024.0f;
+    a.cull_abs = c->scene_extent * 1e-4f;
+    const bool refwalk = (p->flags & PT_FLAG_REFERENCE_TRAVERSAL) != 0;
+    const bool count = (p->flags & PT_FLAG_COUNT) != 0;
+    const uint32_t levels = (uint32_t)c->depth + 2;
+    a.stack_words = levels * 128;
+    const size_t lds = (size_t)a.stack_words * 4;
+    if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
+
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
+    const uint32_t waves_per_cu = 16;
+    uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
+    if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
+    HIP_TRY(hipEventRecord(c->ev0, stream));
+    if (p->spp > 0 && a.ntiles_shard > 0) {
+#define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
+        if (p->integrator == PT_INTEGRATOR_HEAD) {
+            if (refwalk) { if (count) PT_LAUNCH(1, true, true); else PT_LAUNCH(1, true, false); }
+            else { if (count) PT_LAUNCH(1, false, true); else PT_LAUNCH(1, false, false); }
+        } else {
+            if (refwalk) { if (count) PT_LAUNCH(0, true, true); else PT_LAUNCH(0, true, false); }
+            else { if (count) PT_LAUNCH(0, false, true); else PT_LAUNCH(0, false, false); }
+        }
+#undef PT_LAUNCH
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev1, stream));
+    unsigned long long cnt[8];
+    HIP_TRY(hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (st) {
+        st->seconds = ms * 1e-3;
+        st->kernel_ms = ms;
+        st->rays_traced = cnt[0];
+        st->rays_reference = cnt[1];
+        st->node_tests = cnt[2];
+        st->tri_tests = cnt[3];
+        st->samples = cnt[4];
+        const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
+        st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
+    }
+    return PT_OK;
+}
+
+int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rgb, pt_stats* st)
+{
+    if (!c || !p || !out_rgb) return pt::fail(PT_E_INVALID, "pt_render: null argument");
+    if (p->width <= 0 || p->height <= 0) return pt::fail(PT_E_INVALID, "pt_render: bad image size");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = (size_t)p->width * (size_t)p->height * 3 * sizeof(float);
+    if (c->scratch_bytes < bytes) {
+        if (c->scratch_out) (void)hipFree(c->scratch_out);
+        c->scratch_out = nullptr;
+        c->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->scratch_out), bytes));
+        c->scratch_bytes = bytes;
+    }
+    HIP_TRY(hipMemset(c->scratch_out, 0, bytes));
+    int rc = pt_render_device(c, p, cam, c->scratch_out, nullptr, st);
+    if (rc != PT_OK) return rc;
+    HIP_TRY(hipMemcpy(out_rgb, c->scratch_out, bytes, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+}  // extern "C"

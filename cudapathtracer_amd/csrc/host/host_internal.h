@@ -1,0 +1,72 @@
+// host_internal.h -- shared declarations of the host surface (plain C++17, no HIP).
+#pragma once
+
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pt/pt.h"
+
+static_assert(sizeof(pt_vec3) == 12, "vec3 is 12 B (vec3.h:4-7)");
+static_assert(sizeof(pt_triangle) == 28, "triangle is 28 B (modelLoader.h:14-19)");
+static_assert(sizeof(pt_material) == 48, "materialDesc is 48 B (modelLoader.h:21-25)");
+static_assert(sizeof(pt_bvh_node) == 32, "BVH_array_node is 32 B (BVH.h:111-115)");
+static_assert(sizeof(pt_camera) == 32, "camera is 32 B (camera.h:26-34)");
+
+namespace pt {
+
+// Thread-local error channel behind pt_last_error().
+int fail(int code, const char* fmt, ...);
+void clear_error();
+
+// ---- OBJ/MTL ingest with tinyobj 0.9.13 semantics (tiny_obj_loader.cc) ------------------
+// Only what loadOBJ (modelLoader.h:125-210) consumes is kept: positions, per-triangle
+// indices, per-triangle material ids, material diffuse/emission.  Vertex dedupe keys still
+// include the vt/vn indices, since they decide how many positions a shape gets.
+struct ObjMaterial {
+    std::string name;
+    float diffuse[3];
+    float emission[3];
+};
+struct ObjShape {
+    std::string name;
+    std::vector<float> positions;       // xyz per deduplicated vertex
+    std::vector<uint32_t> indices;      // 3 per triangle
+    std::vector<int> material_ids;      // 1 per triangle
+};
+struct ObjResult {
+    std::vector<ObjShape> shapes;
+    std::vector<ObjMaterial> materials;
+    std::string message;                // tinyobj's returned error/warning string
+    bool fatal = false;                 // file could not be opened / malformed index
+};
+ObjResult read_obj(const std::string& path, const std::string& mtl_basepath);
+
+// Greedy decimal parser of tinyobj's tryParseDouble (tiny_obj_loader.cc:127-241).
+bool parse_real(const char* s, const char* end, double* out);
+
+// ---- scene (the reference's globals, modelLoader.h:43-47) -------------------------------
+struct HostScene {
+    std::vector<pt_vec3> verts;
+    std::vector<pt_triangle> tris;
+    std::vector<pt_material> mats;
+    std::vector<uint32_t> lights;
+    float total_light_area = 0.0f;
+    std::vector<pt_bvh_node> bvh;
+    int32_t bvh_depth = 0;
+    std::string warning;
+};
+
+// Deterministic float sin/cos shared with the kernels (defined in hip/pt_render.hip).
+void sincos_det(float theta, float* s, float* c);
+
+// ---- BVH (BVH.h) ------------------------------------------------------------------------
+int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,
+              std::vector<pt_bvh_node>* out, int32_t* depth);
+
+}  // namespace pt
+
+struct pt_host_scene {
+    pt::HostScene s;
+};

@@ -1,0 +1,174 @@
+/*
+ * pt.h -- C-ABI of the MI355X-native path tracer (libptamd.so).
+ *
+ * Drop-in boundary for CulDeVu/CUDAPathTracer's render call.  Plain C types,
+ * plain pointers and sizes; no torch, no HIP types in any signature.
+ *
+ * Two halves:
+ *   1. Host surface (plain C++ behind C entry points), the reference's callers of the path:
+ *        pt_scene_*      <- modelLoader.h:43-47 globals + loadOBJ (modelLoader.h:125-210)
+ *                           via tinyobj::LoadObj (tiny_obj_loader.cc:638-884)
+ *        pt_scene_build_bvh <- buildBVH (BVH.h:443-474) + depth guard (kernel.cu:627-631)
+ *        pt_camera_ray / pt_morton_* <- camera.h:36-97
+ *        pt_write_ppm    <- kernel.cu:763-778 + color.h:59-71
+ *   2. Render (hand-written gfx950 HIP kernels):
+ *        pt_create       <- the uploads of kernel.cu:637-700 (scene, camera, BVH to device)
+ *        pt_render       <- setupCurand (kernel.cu:527-533, :639) + setupImgBuffer (:520-526, :662)
+ *                           + the NUM_SAMPLES-1 launches of drawPixel (kernel.cu:535-553, :709-736)
+ *        pt_destroy      <- cudaFree (kernel.cu:782-783)
+ *        pt_last_error   <- checkError (kernel.cu:37-42), but returned instead of printed
+ *
+ * Errors: every int-returning entry point returns PT_OK (0) or a negative PT_E* code and
+ * records a message for pt_last_error() (thread-local).  Nothing calls exit().
+ * Ownership: the caller owns every array it passes; pt_create copies what it needs and keeps
+ * no pointer into caller memory.  A pt_ctx is used by one host thread at a time.
+ */
+#ifndef PT_PT_H
+#define PT_PT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+/* ---- status codes */
+#define PT_OK 0
+#define PT_E_INVALID (-1)    /* bad argument                                              */
+#define PT_E_IO (-2)         /* cannot open / read / write a file                          */
+#define PT_E_SCENE (-3)      /* scene unusable (fewer than 2 triangles, bad indices, ...)  */
+#define PT_E_BVH_DEPTH (-4)  /* BVH depth >= 64 (kernel.cu:627-631 "BVH depth is too big") */
+#define PT_E_HIP (-5)        /* HIP runtime error (message names the call)                 */
+#define PT_E_NODEV (-6)      /* no gfx950 device / device index out of range               */
+#define PT_E_OOM (-7)
+
+/* ---- POD mirrors of the reference layouts (static_assert'ed in the implementation) */
+typedef struct { float x, y, z; } pt_vec3;                                      /* vec3.h:4-7, 12 B       */
+typedef struct { int32_t v0, v1, v2; pt_vec3 norm; int32_t mat; } pt_triangle; /* modelLoader.h:14-19, 28 B */
+typedef struct { double albedo[3]; double emission[3]; } pt_material;          /* modelLoader.h:21-25, 48 B */
+typedef struct { pt_vec3 lo, hi; uint32_t left, right; } pt_bvh_node;          /* BVH.h:111-115, 32 B    */
+typedef struct {                                                                /* camera.h:26-34, 32 B   */
+    pt_vec3 pos;
+    float dist_from_film;
+    float focal_length;
+    float radius;
+    int32_t pxl_width, pxl_height;
+} pt_camera;
+
+#define PT_BVH_LEAF_FLAG 0x80000000u   /* limits.h:6 */
+#define PT_MAX_BVH_DEPTH 64            /* kernel.cu:35 */
+
+/* Read-only view of a scene: sceneDesc (modelLoader.h:29-41) + BVH_array (BVH.h:116-121). */
+typedef struct {
+    uint32_t num_verts, num_tris, num_mats, num_lights;
+    const pt_vec3* verts;
+    const pt_triangle* tris;
+    const pt_material* mats;
+    const uint32_t* lights;
+    float total_light_area;
+    const pt_bvh_node* bvh;    /* breadth-first array, node 0 = root            */
+    uint32_t bvh_size;         /* = num_tris - 1                                 */
+    int32_t bvh_depth;         /* BVH_node::depth of the root (BVH.h:322, :346)  */
+} pt_scene;
+
+/* ======================================================================= host surface */
+typedef struct pt_host_scene pt_host_scene;
+
+/* Empty scene (the reference's global vectors, modelLoader.h:43-47, as an object). */
+pt_host_scene* pt_scene_new(void);
+void pt_scene_free(pt_host_scene* s);
+
+/* loadOBJ(filename, origin, scale, flipNormals) -- modelLoader.h:125-210.  Appends to the
+ * scene exactly as the reference appends to its globals.  mtl_basepath: the directory
+ * prefix tinyobj prepends to `mtllib` names (the reference hard-codes "models/",
+ * modelLoader.h:132); NULL means "models/".  A tinyobj warning/error (e.g. a missing .mtl,
+ * which makes tinyobj stop reading the OBJ at the mtllib line) does not fail the call, as in
+ * the reference: it is returned through pt_scene_last_warning(). */
+int pt_scene_load_obj(pt_host_scene* s, const char* obj_path, const char* mtl_basepath,
+                      pt_vec3 origin, float scale, int flip_normals);
+const char* pt_scene_last_warning(const pt_host_scene* s);
+
+/* buildBVH() -- BVH.h:443-474, byte-identical node array.  Fails with PT_E_SCENE for
+ * fewer than 2 triangles (decision d5) and PT_E_BVH_DEPTH when depth >= 64. */
+int pt_scene_build_bvh(pt_host_scene* s);
+
+/* Borrow a view of the scene arrays (valid until the next mutation or pt_scene_free). */
+int pt_scene_view(const pt_host_scene* s, pt_scene* out);
+
+/* camera.h:57-75 Morton maps and camera.h:77-97 cameraRay.  `lens` = 0: no lens draws
+ * (exactly zero lens offset); otherwise (u1,u2) are the lens draws. */
+uint32_t pt_morton_pxl_to_i(uint32_t x, uint32_t y);
+void pt_morton_i_to_pxl(uint32_t idx, uint32_t* x, uint32_t* y);
+void pt_camera_ray(const pt_camera* cam, uint32_t idx, int lens, float u1, float u2,
+                   pt_vec3* origin, pt_vec3* dir);
+
+/* kernel.cu:763-778: "P3 W H 255\n" then "%d %d %d " for rows y = 0..H-1 and x = W-1..0,
+ * c = (int)(pow(c/(c+1), (float)(1/2.2)) * 255).  rgb is the scanline mean buffer written by
+ * pt_render (pixel (x,y) at rgb[(y*W + x)*3]); the f64 variant takes the reference's own
+ * double accumulator type. */
+int pt_write_ppm(const char* path, const float* rgb, int width, int height);
+int pt_write_ppm_f64(const char* path, const double* rgb, int width, int height);
+/* PPM tone map of one value: (int)(pow(c/(c+1), (double)(float)(1/2.2)) * 255). */
+int pt_tonemap_u8(double c);
+
+/* ============================================================================ render */
+typedef struct pt_ctx pt_ctx;
+
+#define PT_INTEGRATOR_UNIDIR 0   /* radianceAlongSingleStep2, kernel.cu:417-515 (north star) */
+#define PT_INTEGRATOR_HEAD 1     /* radianceAlongSingleStep,  kernel.cu:217-415 (HEAD :549)  */
+
+/* pt_params.flags */
+#define PT_FLAG_REFERENCE_TRAVERSAL 0x1u  /* left-first stack walk with no distance culling,
+                                             the exact node/triangle sequence of kernel.cu:112-161 */
+#define PT_FLAG_NO_DEAD_PATH_SKIP 0x2u    /* trace every bounce even after the path weight is 0   */
+#define PT_FLAG_NO_PRIMARY_CACHE 0x4u     /* re-trace the (sample-invariant) camera ray per sample  */
+#define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant)     */
+
+typedef struct {
+    int32_t width, height;   /* image size (IMAGE_WIDTH/HEIGHT, kernel.cu:28-29)                    */
+    int32_t spp;             /* samples per pixel = the reference's NUM_SAMPLES - 1 (kernel.cu:709) */
+    int32_t bounces;         /* NUM_BOUNCES (kernel.cu:33), integrator 0 only, 1..64                 */
+    int32_t integrator;      /* PT_INTEGRATOR_*                                                     */
+    uint32_t flags;          /* PT_FLAG_*                                                           */
+    uint64_t seed;           /* curand_init seed (kernel.cu:532 uses 1234)                          */
+    int32_t shard_index;     /* this renderer's shard in [0, shard_count)                           */
+    int32_t shard_count;     /* image tiles (8x8) are dealt round-robin: tile t -> shard t % count  */
+} pt_params;
+
+typedef struct {
+    double seconds;            /* device time of the render kernels (hipEvent pair)              */
+    double kernel_ms;          /* same, in ms, of the dominant (integration) kernel               */
+    uint64_t samples;          /* pixel samples computed                                         */
+    uint64_t rays_traced;      /* trace() calls actually executed on the device                   */
+    uint64_t rays_reference;   /* trace() calls the reference integrator performs for the same
+                                  samples (differs from rays_traced by the primary-ray cache and
+                                  the dead-path skip)                                             */
+    uint64_t rays_nominal;     /* W*H*spp*(bounces+1): the kernel.cu:757 formula, in 64-bit       */
+    uint64_t node_tests;       /* box tests (PT_FLAG_COUNT only)                                  */
+    uint64_t tri_tests;        /* triangle tests (PT_FLAG_COUNT only)                             */
+} pt_stats;
+
+/* Upload a scene to HIP device `device` (ordinal among visible devices). */
+pt_ctx* pt_create(const pt_scene* scene, int device, int* err);
+
+/* Render into a HOST buffer out_rgb[W*H*3] (fp32 mean radiance, scanline order).  Pixels
+ * outside this shard are written as 0.  Blocking. */
+int pt_render(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float* out_rgb, pt_stats* stats);
+
+/* Same into a DEVICE buffer d_out[W*H*3] on `stream` (a hipStream_t, NULL = default stream).
+ * Only this shard's pixels are written; the caller zero-fills the buffer (a multi-GPU job
+ * then sums the shards with one RCCL reduce).  Blocking (it waits for its own events). */
+int pt_render_device(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float* d_out,
+                     void* stream, pt_stats* stats);
+
+void pt_destroy(pt_ctx* ctx);
+const char* pt_last_error(void);
+int pt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,169 @@
+// refgen.cpp -- golden-vector generator built from the REFERENCE's own sources.
+//
+// TEST INFRASTRUCTURE ONLY.  The reference headers are #included in place from
+// /root/reference (nothing is copied into this repo).  The only adaptation is on the
+// command line / below: CUDA's function-space qualifiers __host__/__device__ are
+// defined empty (a host compile), and min/max/abs are brought in from <algorithm>/<cmath>
+// as the reference's nvcc build got them from CUDA's math headers.  No header,
+// library or generated file is substituted.  kernel.cu itself is NOT built (it needs
+// cuda_runtime.h, cuRAND, NVML, windows.h and the broken triple.h -- see DESIGN.md).
+//
+// Built by oracle/Makefile into oracle/_ref/refgen (git-ignored).  Driven by
+// tools/make_golden.py, which writes tests/golden/*.
+//
+// Commands (all binary I/O little-endian, raw arrays):
+//   refgen scene <out_prefix> <obj> <ox> <oy> <oz> <scale> <flip> [<obj> ...]   (cwd = dir holding models/)
+//   refgen tri   <in.bin> <out.bin>   in: n x {o[3], d[3], v0[3], v1[3], v2[3]} f32 ; out: n x f32 t
+//   refgen aabb  <in.bin> <out.bin>   in: n x {o[3], d[3], lo[3], hi[3]} f32     ; out: n x u8
+//   refgen cam   <in.bin> <out.bin>   in: {cam 32 B} + n x {idx u32, u1 f32, u2 f32}; out: n x {o[3], d[3]} f32
+//   refgen morton <out.bin> <n>       out: n x {x u16, y u16, back u32} for idx 0..n-1
+//   refgen tone  <in.bin> <out.bin>   in: n x 3 f64 ; out: n x 3 i32 = (int)(gammaCorrect(normalized(c), 1/2.2)*255)
+#include <cstdint>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <vector>
+#include <string>
+using std::min;
+using std::max;
+using std::abs;
+
+#define __host__
+#define __device__
+#include "/root/reference/modelLoader.h"
+#include "/root/reference/BVH.h"
+#include "/root/reference/camera.h"
+
+static std::vector<char> slurp(const char* path)
+{
+    std::vector<char> buf;
+    FILE* f = fopen(path, "rb");
+    if (!f) { fprintf(stderr, "refgen: cannot open %s\n", path); exit(2); }
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    buf.resize((size_t)n);
+    if (n && fread(buf.data(), 1, (size_t)n, f) != (size_t)n) { fprintf(stderr, "refgen: short read\n"); exit(2); }
+    fclose(f);
+    return buf;
+}
+
+static void spit(const char* path, const void* p, size_t n)
+{
+    FILE* f = fopen(path, "wb");
+    if (!f) { fprintf(stderr, "refgen: cannot write %s\n", path); exit(2); }
+    if (n) fwrite(p, 1, n, f);
+    fclose(f);
+}
+
+static void spit_s(const std::string& path, const void* p, size_t n) { spit(path.c_str(), p, n); }
+
+int main(int argc, char** argv)
+{
+    if (argc < 2) { fprintf(stderr, "usage: refgen <cmd> ...\n"); return 2; }
+    std::string cmd = argv[1];
+    if (cmd == "scene") {
+        std::string pre = argv[2];
+        for (int a = 3; a + 5 < argc; a += 6) {
+            vec3 origin((float)atof(argv[a + 1]), (float)atof(argv[a + 2]), (float)atof(argv[a + 3]));
+            loadOBJ(argv[a], origin, (float)atof(argv[a + 4]), atoi(argv[a + 5]) != 0);   // modelLoader.h:125
+        }
+        spit_s(pre + ".verts.bin", verts.data(), verts.size() * sizeof(vec3));
+        spit_s(pre + ".tris.bin", tris.data(), tris.size() * sizeof(triangle));
+        spit_s(pre + ".mats.bin", mats.data(), mats.size() * sizeof(materialDesc));
+        spit_s(pre + ".lights.bin", lights.data(), lights.size() * sizeof(int32_t));
+        float tla = totalLightArea;
+        int32_t bvh_size = 0, bvh_depth = 0;
+        if (tris.size() >= 2) {
+            BVH_array bvh = buildBVH();                                                  // BVH.h:443
+            bvh_size = bvh.size;
+            bvh_depth = bvh.depth;
+            spit_s(pre + ".bvh.bin", bvh.root, (size_t)bvh.size * sizeof(BVH_array_node));
+        } else {
+            spit_s(pre + ".bvh.bin", nullptr, 0);
+        }
+        FILE* f = fopen((pre + ".meta.txt").c_str(), "w");
+        fprintf(f, "%zu %zu %zu %zu %.9g %a %d %d\n", verts.size(), tris.size(), mats.size(), lights.size(),
+                (double)tla, (double)tla, bvh_size, bvh_depth);
+        fclose(f);
+        return 0;
+    }
+    if (cmd == "tri") {
+        std::vector<char> in = slurp(argv[2]);
+        size_t n = in.size() / (15 * 4);
+        const float* p = (const float*)in.data();
+        std::vector<float> out(n);
+        for (size_t i = 0; i < n; ++i) {
+            const float* r = p + i * 15;
+            vec3 vs[3] = {vec3(r[6], r[7], r[8]), vec3(r[9], r[10], r[11]), vec3(r[12], r[13], r[14])};
+            triangle t;
+            t.v0 = 0; t.v1 = 1; t.v2 = 2; t.mat = 0;
+            out[i] = triIntersect(vec3(r[0], r[1], r[2]), vec3(r[3], r[4], r[5]), vs, &t);  // modelLoader.h:49
+        }
+        spit(argv[3], out.data(), n * 4);
+        return 0;
+    }
+    if (cmd == "aabb") {
+        std::vector<char> in = slurp(argv[2]);
+        size_t n = in.size() / (12 * 4);
+        const float* p = (const float*)in.data();
+        std::vector<uint8_t> out(n);
+        for (size_t i = 0; i < n; ++i) {
+            const float* r = p + i * 12;
+            AABB b;
+            b.lo = vec3(r[6], r[7], r[8]);
+            b.hi = vec3(r[9], r[10], r[11]);
+            out[i] = rayAABBIntersect(vec3(r[0], r[1], r[2]), vec3(r[3], r[4], r[5]), b) ? 1 : 0;  // BVH.h:51
+        }
+        spit(argv[3], out.data(), n);
+        return 0;
+    }
+    if (cmd == "cam") {
+        std::vector<char> in = slurp(argv[2]);
+        camera cam;
+        memcpy(&cam, in.data(), sizeof(camera));
+        size_t n = (in.size() - sizeof(camera)) / 12;
+        const char* q = in.data() + sizeof(camera);
+        std::vector<float> out(n * 6);
+        for (size_t i = 0; i < n; ++i) {
+            uint32_t idx; float u1, u2;
+            memcpy(&idx, q + i * 12, 4); memcpy(&u1, q + i * 12 + 4, 4); memcpy(&u2, q + i * 12 + 8, 4);
+            ray r = cam.cameraRay((int)idx, u1, u2);                                         // camera.h:77
+            out[i * 6 + 0] = r.o.x; out[i * 6 + 1] = r.o.y; out[i * 6 + 2] = r.o.z;
+            out[i * 6 + 3] = r.dir.x; out[i * 6 + 4] = r.dir.y; out[i * 6 + 5] = r.dir.z;
+        }
+        spit(argv[3], out.data(), out.size() * 4);
+        return 0;
+    }
+    if (cmd == "morton") {
+        int n = atoi(argv[3]);
+        camera cam;
+        std::vector<uint32_t> out((size_t)n * 2);
+        for (int i = 0; i < n; ++i) {
+            uint16_t x, y;
+            cam.mortonItoPxl(&x, &y, (uint32_t)i);                                          // camera.h:57
+            out[(size_t)i * 2] = (uint32_t)x | ((uint32_t)y << 16);
+            out[(size_t)i * 2 + 1] = cam.mortonPxltoI(x, y);                                 // camera.h:66
+        }
+        spit(argv[2], out.data(), out.size() * 4);
+        return 0;
+    }
+    if (cmd == "tone") {
+        std::vector<char> in = slurp(argv[2]);
+        size_t n = in.size() / 24;
+        const double* p = (const double*)in.data();
+        std::vector<int32_t> out(n * 3);
+        for (size_t i = 0; i < n; ++i) {
+            color c = gammaCorrect(normalized(color(p[i * 3], p[i * 3 + 1], p[i * 3 + 2])), 1 / 2.2);  // kernel.cu:771
+            out[i * 3 + 0] = (int)(c.r * 255);
+            out[i * 3 + 1] = (int)(c.g * 255);
+            out[i * 3 + 2] = (int)(c.b * 255);
+        }
+        spit(argv[3], out.data(), out.size() * 4);
+        return 0;
+    }
+    fprintf(stderr, "refgen: unknown command %s\n", cmd.c_str());
+    return 2;
+}
