@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark of the per-pixel path-integration hot path (BASELINE.json north star).
+
+Workload (config C3): the ~262K-triangle procedural Sponza-class STAND-IN (Sponza is absent
+from this container; PT_SPONZA_OBJ=<path> uses a real file), 1920x1080, 256 spp, 3 bounces,
+unidirectional integrator (kernel.cu:417-515), seed 1234.  One "step" = one full render of
+that image (all samples), inputs resident in HBM; for N GPUs each rank renders its interleaved
+8x8 tiles into a zero-filled fp32 framebuffer and rank 0 receives the RCCL sum (weak scaling
+of the per-GPU work is NOT used: total work per step is fixed, so scaling is "strong").
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with:
+  value      = Msamples/s, whole job (pixel samples per second)
+  roofline   = algorithmic bytes of the render kernel / its measured duration vs 8 TB/s HBM
+  cpu_baseline = the CPU oracle (same integrator) on a bounded pixel subset, host cores
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def scene_path(cache_dir):
+    real = os.environ.get("PT_SPONZA_OBJ")
+    if real:
+        return real, os.path.dirname(real) + "/", "sponza (PT_SPONZA_OBJ)"
+    from cudapathtracer_amd import scenes
+    p = os.path.join(cache_dir, "models", "sponza_standin.obj")
+    if not os.path.exists(p):
+        scenes.write_sponza_standin(cache_dir)
+    return p, os.path.dirname(p) + "/", "sponza_standin_262k (procedural stand-in, not Sponza)"
+
+
+def load(path, mtl):
+    import cudapathtracer_amd as pt
+    t = time.time()
+    s = pt.Scene()
+    s.load_obj(path, mtl_basepath=mtl)
+    s.build_bvh()
+    log("scene loaded + BVH built in %.2fs" % (time.time() - t))
+    return s
+
+
+def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
+    """Oracle (CPU restatement of the same integrator) on a bounded subset of the same image."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from cudapathtracer_amd import shard
+    osc = oracle.OracleScene(scene.arrays())
+    ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"],
+                         width, height)
+    ntiles = shard.tiles_shape(width, height)[0] * shard.tiles_shape(width, height)[1]
+    # calibrate on one tile, then size the subset (every k-th tile, full spp) to the budget
+    t0 = time.time()
+    cal_pix = shard.tile_pixels(width, height, np.array([ntiles // 2]))
+    oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=cal_pix, threads=threads)
+    dt = max(time.time() - t0, 1e-3)
+    tiles_fit = max(1, int(budget_s / dt))
+    stride = max(1, ntiles // tiles_fit)
+    tiles = np.arange(stride // 2, ntiles, stride)[:tiles_fit]
+    pix = shard.tile_pixels(width, height, tiles)
+    t0 = time.time()
+    _, cnt = oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=pix, threads=threads)
+    dt = time.time() - t0
+    samples = len(pix) * spp
+    return {
+        "value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+        "mrays_per_s": cnt["traces"] / dt / 1e6,
+        "sample": "%d pixels (every %d-th 8x8 tile) x %d spp of the same %dx%d image, %.1fs"
+                  % (len(pix), stride, spp, width, height, dt),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--integrator", type=int, default=0)
+    ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--no-count", action="store_true", help="skip the counting pass (roofline bytes)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import cudapathtracer_amd as pt
+    from cudapathtracer_amd import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    os.makedirs(args.cache_dir, exist_ok=True)
+    path, mtl, scene_name = scene_path(args.cache_dir)
+    scene = load(path, mtl)
+    cam_kw = dict(scenes.SPONZA_STANDIN_CAMERA)
+    W, H = args.width, args.height
+    cam = pt.make_camera(width=W, height=H, **cam_kw)
+    r = pt.Renderer(scene, device=local)
+    fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        fb.zero_()
+        st = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
+                             flags=args.flags, shard_index=rank, shard_count=world, stream_ptr=stream)
+        if distributed:
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    # counting pass (same inputs, counting variant): algorithmic bytes of the render kernel
+    counts = None
+    if not args.no_count:
+        fb.zero_()
+        counts = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces,
+                                 integrator=args.integrator, flags=args.flags | pt.PT_FLAG_COUNT,
+                                 shard_index=rank, shard_count=world, stream_ptr=stream)
+    for _ in range(args.warmup):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    stats = []
+    for _ in range(args.steps):
+        st = step()
+        kernel_ms.append(st["kernel_ms"])
+        stats.append(st)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([sum(s["samples"] for s in stats), sum(s["rays_traced"] for s in stats),
+                        sum(s["rays_reference"] for s in stats)], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(t.item())
+    samples, traced, refrays = [float(v) for v in tot.tolist()]
+
+    if rank == 0:
+        img = fb.cpu().numpy()
+        finite = bool(np.isfinite(img).all())
+        ms_step = elapsed / args.steps * 1e3
+        kms = float(np.mean(kernel_ms))
+        roof = None
+        if counts is not None:
+            # algorithmic bytes per launch: 64-B node records fetched + 48-B triangle records tested
+            # + per traced ray 16 B shading record + 48 B material + 12 B/pixel output
+            npx = counts["samples"] / max(args.spp, 1)
+            bytes_launch = (counts["node_tests"] * 64 + counts["tri_tests"] * 48 +
+                            counts["rays_traced"] * (16 + 48) + npx * 12)
+            achieved = bytes_launch / (kms * 1e-3) / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    tj = json.load(open(args.traffic_json))
+                    if tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, world]:
+                        traffic = tj.get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_tiles",
+                    "kernel_ms": round(kms, 3),
+                    "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"])}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget)
+        out = {
+            "metric": "Mrays/sec + Msamples/sec, Sponza 1080p 256spp, 1/2/4/8 GPU",
+            "value": round(samples / elapsed / 1e6, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32 geometry / f64 radiance",
+            "data": "synthetic",
+            "config": {"workload": "C3 %s %dx%d %dspp %d bounces integrator=%d" % (
+                scene_name, W, H, args.spp, args.bounces, args.integrator),
+                "scene": scene_name, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
+                "integrator": "unidirectional" if args.integrator == 0 else "head", "seed": 1234,
+                "parallelism": "image tiles %dx, RCCL reduce" % world if distributed else "1 GPU"},
+            "mrays_per_s_traced": round(traced / elapsed / 1e6, 3),
+            "mrays_per_s_reference_equiv": round(refrays / elapsed / 1e6, 3),
+            "mrays_per_s_nominal": round(samples * (args.bounces + 1) / elapsed / 1e6, 3),
+            "image_finite": finite,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    r.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -242,7 +242,8 @@ struct Hit {
 };
 
 struct Counters {
-    uint32_t nodes, tris;
+    uint32_t nodes;   // node records fetched (64 B culled walk, 32 B reference walk)
+    uint32_t tris;    // triangle records tested (48 B)
 };
 
 // kernel.cu:112-161 trace(): the reference's exact walk -- left child first, every box the
@@ -304,7 +305,6 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
     uint32_t best_slot = 0u;
     uint32_t best_id = 0xffffffffu;
     float ti, to;
-    if (kCount) ++cnt.nodes;
     if (!slab_ref(o, d, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) || to < -cull_abs) {
         Hit h; h.tri = -1; h.t = kMaxFloat; return h;
     }
@@ -314,6 +314,7 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
         const DNode* nd = nodes + node;
         const float4 A = nd->a, B = nd->b, C = nd->c;
         const uint4 D = nd->d;
+        if (kCount) ++cnt.nodes;   // one 64-B record fetched
         bool h0 = false, h1 = false;
         float t0 = 0.0f, t1 = 0.0f;
         if (D.x & kLeaf) {
@@ -324,7 +325,6 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
             if (0.0f < t && (t < best_t || (t == best_t && slot < best_slot))) { best_t = t; best_slot = slot; best_id = id; }
         } else {
             const bool hit = slab_ref(o, d, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to);
-            if (kCount) ++cnt.nodes;
             h0 = hit && !(to < -cull_abs) && !(ti > best_t * cull_rel);
             t0 = ti;
         }
@@ -338,7 +338,6 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
             h0 = h0 && !(t0 > best_t * cull_rel);
         } else {
             const bool hit = slab_ref(o, d, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to);
-            if (kCount) ++cnt.nodes;
             h1 = hit && !(to < -cull_abs) && !(ti > best_t * cull_rel);
             t1 = ti;
         }

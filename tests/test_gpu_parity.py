@@ -1,0 +1,159 @@
+"""gfx950 render path vs the CPU oracle (kernel.cu:417-515 / 217-415 restated), through the C-ABI.
+
+Bar: bit-exact.  The kernel and the oracle implement one arithmetic spec -- IEEE
+float/double ops in the reference's order, no contraction, correctly rounded '/' and sqrt,
+the same deterministic sin/cos -- so the fp32 image the kernel writes must equal the oracle's
+f64 mean rounded to fp32 in every bit, for every traversal/skip/cache mode.  The north-star
+tolerance (RMSE <= 1e-4 on c/(c+1), pixel 0 excluded) is checked as well, at sizes where only
+properties can be checked.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, load_scene
+
+import cudapathtracer_amd as pt
+from cudapathtracer_amd import shard
+
+pytestmark = pytest.mark.gpu
+
+CAM = dict(pos=(0.0, 1.0, 3.0), dist_from_film=1.0, focal_length=3.0, radius=0.0)   # kernel.cu:642-648
+
+
+@pytest.fixture(scope="module")
+def oracle_mod():
+    import oracle
+    return oracle
+
+
+@pytest.fixture(scope="module")
+def cb():
+    s = load_scene("cornell_blob")
+    r = pt.Renderer(s, 0)
+    yield s, r
+    r.close()
+
+
+def _oracle(oracle_mod, scene, w, h, spp, bounces, integ, seed=1234, radius=0.0, pixels=None):
+    osc = oracle_mod.OracleScene(scene.arrays())
+    ocam = oracle_mod.camera(CAM["pos"], CAM["dist_from_film"], CAM["focal_length"], radius, w, h)
+    img, cnt = oracle_mod.render(osc, ocam, w, h, spp, bounces, integ, seed, pixels=pixels)
+    return img, cnt
+
+
+def _bits_equal(a32, ref64):
+    return int(np.count_nonzero(a32.view(np.uint32) != ref64.astype(np.float32).view(np.uint32)))
+
+
+def _rmse_tonemapped(a, b):
+    a = a.astype(np.float64).reshape(-1, 3)[1:]
+    b = b.astype(np.float64).reshape(-1, 3)[1:]
+    return float(np.sqrt(np.mean((a / (a + 1) - b / (b + 1)) ** 2)))
+
+
+MODES = [0, pt.PT_FLAG_REFERENCE_TRAVERSAL, pt.PT_FLAG_NO_DEAD_PATH_SKIP | pt.PT_FLAG_NO_PRIMARY_CACHE,
+         pt.PT_FLAG_REFERENCE_TRAVERSAL | pt.PT_FLAG_NO_DEAD_PATH_SKIP, pt.PT_FLAG_COUNT]
+
+
+@pytest.mark.parametrize("flags", MODES)
+@pytest.mark.parametrize("integ", [0, 1])
+def test_bit_exact_vs_oracle(oracle_mod, cb, integ, flags):
+    s, r = cb
+    w, h, spp = 32, 32, 4
+    img, st = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=3, integrator=integ,
+                       flags=flags)
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, integ)
+    assert _bits_equal(img, ref) == 0
+    assert st["samples"] == w * h * spp
+    # the reference's own trace count is reproduced exactly (traced <= reference)
+    assert st["rays_reference"] == cnt["traces"]
+    assert st["rays_traced"] <= st["rays_reference"]
+    if flags & pt.PT_FLAG_NO_DEAD_PATH_SKIP and flags & pt.PT_FLAG_NO_PRIMARY_CACHE:
+        assert st["rays_traced"] == cnt["traces"]
+    if flags & pt.PT_FLAG_COUNT:
+        assert st["node_tests"] > 0 and st["tri_tests"] > 0
+
+
+def test_matches_committed_fixture(cb):
+    """The committed oracle render (tests/golden) pins both sides across rebuilds."""
+    s, r = cb
+    for integ in (0, 1):
+        g = np.load(os.path.join(GOLD, "render_cornell_blob_32x32_s4_b3_i%d.npz" % integ))
+        img, _ = r.render(pt.make_camera(width=32, height=32, **CAM), 32, 32, 4, bounces=3, integrator=integ)
+        assert _bits_equal(img, g["img"]) == 0
+
+
+@pytest.mark.parametrize("w,h,spp,bounces", [(24, 16, 3, 8), (13, 7, 5, 1), (1, 1, 3, 3), (40, 9, 2, 16)])
+def test_ragged_images_and_depths(oracle_mod, w, h, spp, bounces):
+    """Non-square, non-power-of-two and tile-ragged images (decision d3), depth 1..16."""
+    s = load_scene("cornell")
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=bounces)
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, bounces, 0)
+    assert _bits_equal(img, ref) == 0
+    assert st["rays_reference"] == cnt["traces"]
+
+
+def test_lens_radius_and_seed(oracle_mod, cb):
+    """radius > 0 consumes the two lens draws per sample from the pixel's stream (decision d1)."""
+    s, r = cb
+    w, h = 16, 16
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=0.05, width=w, height=h)
+    img, _ = r.render(cam, w, h, 3, bounces=3, seed=99)
+    ref, _ = _oracle(oracle_mod, s, w, h, 3, 3, 0, seed=99, radius=0.05)
+    assert _bits_equal(img, ref) == 0
+
+
+def test_shards_sum_to_full_render(cb):
+    """Tile sharding: every shard writes only its tiles and the sum is bit-identical."""
+    s, r = cb
+    w, h, spp = 40, 24, 2
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    full, st = r.render(cam, w, h, spp)
+    for n in (2, 3, 8):
+        acc = np.zeros_like(full)
+        tot = 0
+        for k in range(n):
+            part, stk = r.render(cam, w, h, spp, shard_index=k, shard_count=n)
+            mask = np.zeros(w * h, dtype=bool)
+            mask[shard.shard_pixels(w, h, k, n)] = True
+            assert np.all(part.reshape(-1, 3)[~mask] == 0)
+            acc += part
+            tot += stk["samples"]
+        assert _bits_equal(acc, full.astype(np.float64)) == 0
+        assert tot == st["samples"]
+
+
+def test_rmse_and_properties_larger(oracle_mod, cb):
+    """North-star tolerance on a subset of a larger render (oracle only on the subset)."""
+    s, r = cb
+    w = h = 256
+    spp = 8
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    img, st = r.render(cam, w, h, spp, bounces=3)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    pix = shard.shard_pixels(w, h, 5, 97)
+    ref, _ = _oracle(oracle_mod, s, w, h, spp, 3, 0, pixels=pix)
+    a = img.reshape(-1, 3)[pix]
+    b = ref.reshape(-1, 3)[pix]
+    assert _rmse_tonemapped(a, b) <= 1e-4
+    assert int(np.count_nonzero(a.view(np.uint32) != b.astype(np.float32).view(np.uint32))) == 0
+
+
+def test_culled_walk_agrees_with_reference_walk_standin(tmp_path):
+    """On the 262K-triangle stand-in the culled near-first walk returns the reference walk's
+    hits: the two renders must agree bit-for-bit (and so must their reference ray counts)."""
+    from cudapathtracer_amd import scenes
+    p = scenes.write_sponza_standin(str(tmp_path))
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    s.build_bvh()
+    w, h = 96, 64
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    with pt.Renderer(s, 0) as r:
+        a, sa = r.render(cam, w, h, 4, bounces=3)
+        b, sb = r.render(cam, w, h, 4, bounces=3, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
+    assert _bits_equal(a, b.astype(np.float64)) == 0
+    assert sa["rays_reference"] == sb["rays_reference"]
