@@ -235,16 +235,180 @@ __device__ __forceinline__ bool slab_ref(V3 o, V3 d, float lx, float ly, float l
     return true;
 }
 
+struct Counters {
+    uint32_t nodes;   // node records fetched (64 B culled walk, 32 B reference walk)
+    uint32_t tris;    // triangle records tested (48 B)
+};
+
+// ------------------------------------------------------------------ exact division, cheaply
+// Markstein's correction: with y = RN(1/d), q0 = RN(x*y), r = x - d*q0 (exact by FMA),
+// RN(q0 + r*y) == RN(x/d) -- the correctly rounded quotient the reference's '/' produces --
+// whenever nothing under/overflows.  The walks use it only when every numerator is 0 or has
+// magnitude >= 2^-80 and every divisor magnitude lies in [2^-100, 2^45]: guaranteed when all
+// scene coordinates and the ray origin are 0 or in [2^-50, 2^20] and |d_k| >= 2^-100 (checked
+// per scene at pt_create and per ray in ray_fast()); otherwise the wave takes the IEEE '/'
+// path.  Verified bit-exact on 2e9 random pairs over those ranges.
+__device__ __forceinline__ float div_mk(float x, float d, float y)
+{
+    const float q0 = x * y;
+    const float r = __builtin_fmaf(-q0, d, x);
+    return __builtin_fmaf(r, y, q0);
+}
+
+__device__ __forceinline__ bool coord_ok(float v)
+{
+    const float a = __builtin_fabsf(v);
+    return a == 0.0f || (a >= 0x1p-50f && a <= 0x1p20f);
+}
+
+__device__ __forceinline__ bool ray_fast(V3 o, V3 d)
+{
+    return coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && __builtin_fabsf(d.x) >= 0x1p-100f &&
+           __builtin_fabsf(d.y) >= 0x1p-100f && __builtin_fabsf(d.z) >= 0x1p-100f;
+}
+
+// slab test of BVH.h:51-83; kMk selects the Markstein quotient (same bits as '/').
+template <bool kMk>
+__device__ __forceinline__ bool slab(V3 o, V3 d, V3 y, float lx, float ly, float lz, float hx, float hy, float hz,
+                                     float* t_in, float* t_out)
+{
+    float tmin, tmax, tymin, tymax, tzmin, tzmax, tt;
+    if (kMk) {
+        tmin = div_mk(lx - o.x, d.x, y.x); tmax = div_mk(hx - o.x, d.x, y.x);
+        tymin = div_mk(ly - o.y, d.y, y.y); tymax = div_mk(hy - o.y, d.y, y.y);
+        tzmin = div_mk(lz - o.z, d.z, y.z); tzmax = div_mk(hz - o.z, d.z, y.z);
+    } else {
+        tmin = (lx - o.x) / d.x; tmax = (hx - o.x) / d.x;
+        tymin = (ly - o.y) / d.y; tymax = (hy - o.y) / d.y;
+        tzmin = (lz - o.z) / d.z; tzmax = (hz - o.z) / d.z;
+    }
+    if (tmin > tmax) { tt = tmin; tmin = tmax; tmax = tt; }
+    if (tymin > tymax) { tt = tymin; tymin = tymax; tymax = tt; }
+    if (tzmin > tzmax) { tt = tzmin; tzmin = tzmax; tzmax = tt; }
+    *t_in = __builtin_fmaxf(__builtin_fmaxf(tmin, tymin), tzmin);
+    *t_out = __builtin_fminf(__builtin_fminf(tmax, tymax), tzmax);
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    return true;
+}
+
+// triIntersect (modelLoader.h:49-83); kMk: one IEEE reciprocal of `a`, Markstein quotients.
+template <bool kMk>
+__device__ __forceinline__ float tri_hit(V3 o, V3 d, const DTri* __restrict__ tr, uint32_t* id)
+{
+    const float4 A = tr->a, B = tr->b, C = tr->c;
+    *id = __float_as_uint(C.y);
+    const V3 v0 = v3(A.x, A.y, A.z), e1 = v3(A.w, B.x, B.y), e2 = v3(B.z, B.w, C.x);
+    const V3 q = cross(d, e2);
+    const float a = dot(e1, q);
+    if ((double)__builtin_fabsf(a) < 0.00001) return kMaxFloat;
+    const V3 w = o - v0;
+    V3 s;
+    if (kMk) {
+        const float ya = 1.0f / a;
+        s = v3(div_mk(w.x, a, ya), div_mk(w.y, a, ya), div_mk(w.z, a, ya));
+    } else {
+        s = w / a;
+    }
+    const V3 r = cross(s, e1);
+    const float b0 = dot(s, q);
+    const float b1 = dot(r, d);
+    const float b2 = 1.0f - b0 - b1;
+    if (b0 < 0.0f) return kMaxFloat;
+    if (b1 < 0.0f) return kMaxFloat;
+    if (b2 < 0.0f) return kMaxFloat;
+    return dot(e2, r);
+}
+
+// Resumable state of the culled near-first walk (trace_culled below, one node per step).
+struct Walk {
+    V3 o, d, y;           // ray, y = RN(1/d)
+    uint32_t node;        // current node record
+    int32_t sp;           // LDS stack depth
+    float best_t;
+    uint32_t best_slot, best_id;
+};
+
+// Start a walk: root box test (the reference tests node 0's own box first).  Returns false
+// when the ray misses the root (walk finished, no hit).
+template <bool kMk>
+__device__ __forceinline__ bool walk_begin(Walk& w, V3 o, V3 d, const float* root, float cull_abs)
+{
+    w.o = o; w.d = d;
+    w.y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    w.node = 0; w.sp = 0;
+    w.best_t = kMaxFloat; w.best_slot = 0u; w.best_id = 0xffffffffu;
+    float ti, to;
+    return slab<kMk>(o, d, w.y, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) && !(to < -cull_abs);
+}
+
+// One node of the walk.  Returns true while the walk continues.
+template <bool kMk, bool kCount>
+__device__ __forceinline__ bool walk_step(Walk& w, const DNode* __restrict__ nodes, const DTri* __restrict__ tris,
+                                          uint32_t* stack, int lane, float cull_rel, float cull_abs,
+                                          uint32_t node_mask, Counters& cnt)
+{
+    const DNode* nd = nodes + w.node;
+    const float4 A = nd->a, B = nd->b, C = nd->c;
+    const uint4 D = nd->d;
+    if (kCount) ++cnt.nodes;
+    float ti, to, t0 = 0.0f, t1 = 0.0f;
+    bool h0 = false, h1 = false;
+    if (D.x & kLeaf) {
+        const uint32_t slot = D.x ^ kLeaf;
+        uint32_t id;
+        const float t = tri_hit<kMk>(w.o, w.d, tris + slot, &id);
+        if (kCount) ++cnt.tris;
+        if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
+    } else {
+        h0 = slab<kMk>(w.o, w.d, w.y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to) && !(to < -cull_abs) &&
+             !(ti > w.best_t * cull_rel);
+        t0 = ti;
+    }
+    if (D.y & kLeaf) {
+        const uint32_t slot = D.y ^ kLeaf;
+        uint32_t id;
+        const float t = tri_hit<kMk>(w.o, w.d, tris + slot, &id);
+        if (kCount) ++cnt.tris;
+        if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
+        h0 = h0 && !(t0 > w.best_t * cull_rel);
+    } else {
+        h1 = slab<kMk>(w.o, w.d, w.y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to) && !(to < -cull_abs) &&
+             !(ti > w.best_t * cull_rel);
+        t1 = ti;
+    }
+    // LDS stack entry: far child's node index in the low node_bits, the top bits of its entry
+    // distance above them (its float truncated toward zero: a lower bound for t >= 0, so the
+    // pop-time cull stays conservative).  node_bits <= 23 keeps sign and exponent intact.
+    if (h0 && h1) {
+        const bool swap = t1 < t0;
+        const uint32_t far_node = swap ? D.x : D.y;
+        const uint32_t far_t = __float_as_uint(swap ? t0 : t1);
+        stack[w.sp * 64 + lane] = (far_t & ~node_mask) | far_node;
+        ++w.sp;
+        w.node = swap ? D.y : D.x;
+        return true;
+    }
+    if (h0 | h1) { w.node = h0 ? D.x : D.y; return true; }
+    while (w.sp > 0) {
+        --w.sp;
+        const uint32_t e = stack[w.sp * 64 + lane];
+        const float et = __uint_as_float(e & ~node_mask);
+        if (et > w.best_t * cull_rel) continue;
+        w.node = e & node_mask;
+        return true;
+    }
+    return false;
+}
+
 // ------------------------------------------------------------------ traversal results
 struct Hit {
     int32_t tri;     // original triangle id, -1 = miss
     float t;         // closestT (MAX_FLOAT on miss)
 };
 
-struct Counters {
-    uint32_t nodes;   // node records fetched (64 B culled walk, 32 B reference walk)
-    uint32_t tris;    // triangle records tested (48 B)
-};
 
 // kernel.cu:112-161 trace(): the reference's exact walk -- left child first, every box the
 // line overlaps, strict 0 < t < closestT.  The stack lives in LDS (kStack entries per lane,

@@ -48,6 +48,11 @@ struct Args {
     uint32_t tiles_x, ntiles_shard;
     uint32_t stack_words;           // LDS words per wave
     float cull_rel, cull_abs;
+    uint32_t* pixel_counter;        // wavefront kernel: next pixel unit
+    uint32_t nunits;                // ntiles_shard * 64
+    uint32_t scene_fast;            // all scene coordinates admit the Markstein quotient
+    uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
+    uint32_t node_mask;             // low bits of a packed stack entry holding the node index
 };
 
 // ------------------------------------------------------------------ per-lane tracer
@@ -429,6 +434,226 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
     }
 }
 
+// ------------------------------------------------------------------ wavefront kernel
+// Integrator 0 as a per-lane state machine (the persistent "while-while" scheme): each lane owns
+// one pixel at a time and walks through its samples and bounces; the wave alternates between
+// (a) BVH walk steps for the lanes that are tracing, kept running until wf_threshold lanes are
+// waiting, and (b) a shading pass in which every waiting lane consumes its hit, draws its next
+// direction, finishes samples / pixels and fetches new pixels.  Lanes therefore do not idle
+// until the slowest ray of the wave is done, which is where the tile kernel loses most time.
+// Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
+enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3 };
+
+template <bool kCount>
+__global__ __launch_bounds__(256) void render_unidir_wf(Args a)
+{
+    extern __shared__ uint32_t lds_wf[];
+    const int lane = threadIdx.x & 63;
+    uint32_t* stack = lds_wf + (threadIdx.x >> 6) * a.stack_words;
+    const int D = a.bounces;
+    const bool skip_dead = !(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP);
+    const bool memo_on = !(a.flags & PT_FLAG_NO_PRIMARY_CACHE);
+    Counters cnt;
+    cnt.nodes = 0;
+    cnt.tris = 0;
+    uint32_t traced = 0, reference = 0;
+    unsigned long long samples = 0;
+
+    uint32_t state = ST_IDLE;
+    uint32_t px = 0, py = 0;
+    int n = 0;
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    Rng rng;
+    rng.d = rng.v0 = rng.v1 = rng.v2 = rng.v3 = rng.v4 = 0;
+    bool lens = false;
+    bool have = false;
+    uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0, k5 = 0;
+    int32_t mtri = -1;
+    float mt = kMaxFloat;
+    int i = 0;
+    C3 acc = c3(0, 0, 0), wgt = c3(1, 1, 1);
+    V3 ro = v3(0, 0, 0), rd = v3(0, 0, 1);
+    Walk w;
+    bool wfast = false;
+    bool primary = false;     // the pending trace is a camera ray (memo store on completion)
+    int32_t htri = -1;
+    float ht = kMaxFloat;
+    // begin a trace of (o, d); a root miss resolves immediately (returns true = hit known)
+    auto begin_trace = [&](V3 o, V3 d) -> bool {
+        ++traced;
+        wfast = (a.scene_fast != 0u) && ray_fast(o, d);
+        const bool inside = wfast ? walk_begin<true>(w, o, d, a.root, a.cull_abs)
+                                  : walk_begin<false>(w, o, d, a.root, a.cull_abs);
+        if (!inside) { htri = -1; ht = kMaxFloat; return true; }
+        state = ST_TRACE;
+        return false;
+    };
+    // start sample n of the current pixel: camera ray, then memo or trace; true = hit known
+    auto start_sample = [&]() -> bool {
+        i = 0;
+        acc = c3(0, 0, 0);
+        wgt = c3(1, 1, 1);
+        float u1 = 0.0f, u2 = 0.0f;
+        if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
+        camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
+        ++reference;
+        if (memo_on && have && k0 == __float_as_uint(ro.x) && k1 == __float_as_uint(ro.y) &&
+            k2 == __float_as_uint(ro.z) && k3 == __float_as_uint(rd.x) && k4 == __float_as_uint(rd.y) &&
+            k5 == __float_as_uint(rd.z)) {
+            htri = mtri; ht = mt; primary = false;
+            return true;
+        }
+        primary = true;
+        return begin_trace(ro, rd);
+    };
+
+    for (;;) {
+        // ---------------------------------------------------------------- refill
+        const uint64_t idle = __ballot(state == ST_IDLE);
+        if (idle) {
+            const uint32_t need = (uint32_t)__popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.pixel_counter, need);
+            base = __shfl(base, leader, 64);
+            if (state == ST_IDLE) {
+                const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (u >= a.nunits) {
+                    state = ST_DONE;
+                } else {
+                    const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
+                    const uint32_t l = u & 63u;
+                    const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
+                    const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
+                    px = (t % a.tiles_x) * kTile + qx;
+                    py = (t / a.tiles_x) * kTile + qy;
+                    if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
+                        const uint32_t idx = morton2(px, py);
+                        rng_init(rng, a.seed, idx, a.jump);
+                        lens = (idx == 0) || (a.cam.radius != 0.0f);
+                        have = false;
+                        n = 1;
+                        m0 = m1 = m2 = 0.0;
+                        state = ST_SHADE;      // provisional; start_sample sets TRACE if it traces
+                        if (!start_sample()) state = ST_TRACE;
+                    }
+                }
+            }
+        }
+        if (__ballot(state != ST_DONE) == 0ull) break;
+
+        // ---------------------------------------------------------------- walk
+        for (;;) {
+            const uint64_t tracing = __ballot(state == ST_TRACE);
+            if (tracing == 0ull) break;
+            if ((uint32_t)__popcll(__ballot(state == ST_SHADE || state == ST_IDLE)) >= a.wf_threshold) break;
+            const bool allfast = __ballot(state == ST_TRACE && !wfast) == 0ull;
+            if (state == ST_TRACE) {
+                const bool more = allfast
+                    ? walk_step<true, kCount>(w, a.nodes, a.tris_leaf, stack, lane, a.cull_rel, a.cull_abs,
+                                              a.node_mask, cnt)
+                    : walk_step<false, kCount>(w, a.nodes, a.tris_leaf, stack, lane, a.cull_rel, a.cull_abs,
+                                               a.node_mask, cnt);
+                if (!more) {
+                    htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
+                    ht = w.best_t;
+                    state = ST_SHADE;
+                }
+            }
+        }
+
+        // ---------------------------------------------------------------- shade
+        if (state == ST_SHADE) {
+            bool again = true;
+            while (again) {
+                again = false;
+                if (primary && memo_on) {
+                    have = true;
+                    k0 = __float_as_uint(ro.x); k1 = __float_as_uint(ro.y); k2 = __float_as_uint(ro.z);
+                    k3 = __float_as_uint(rd.x); k4 = __float_as_uint(rd.y); k5 = __float_as_uint(rd.z);
+                    mtri = htri; mt = ht;
+                }
+                primary = false;
+                // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
+                {
+                    int32_t tri = htri;
+                    float t = (float)((double)ht - 0.001);
+                    if ((double)t < 0.001) wgt = c3(0, 0, 0);
+                    if (t > kMaxFloat - 1) { wgt = c3(0, 0, 0); tri = 0; t = 0; }
+                    const int32_t mi = ld_mat(a.shade, tri);
+                    const DMat* cm = a.mats + mi;
+                    const V3 normal = ld_norm(a.shade, tri);
+                    const V3 pos = ro + rd * t;
+                    if (cm->emission[0] != 0) {
+                        acc = cadd(acc, cmul(wgt, mat_emission(cm)));
+                        wgt = c3(0, 0, 0);
+                    }
+                    V3 ldir;
+                    const float u = rng_uniform(rng);
+                    if (u < 0.5) {
+                        ldir = cosine_ray(normal, rng);
+                        wgt = cmul(wgt, cmulf(brdf(cm), (float)3.14159));
+                    } else {
+                        V3 p1;
+                        pick_light(a, rng, &p1);
+                        const V3 dd = p1 - pos;
+                        ldir = normalized(dd);
+                        const float cos_l = __builtin_fmaxf(0.0f, dot(ldir, normal));
+                        const float cos_o = __builtin_fmaxf(0.0f, dot(v3(0, -1, 0), ldir * -1));
+                        const float G = cos_l * cos_o / dot(dd, dd);
+                        wgt = cmul(wgt, cmulf(cmulf(brdf(cm), G), a.total_light_area));
+                        i = (i > D - 2) ? i : D - 2;
+                    }
+                    ro = pos;
+                    rd = ldir;
+                    ++i;
+                }
+                // advance to the next trace this lane needs
+                for (;;) {
+                    if (i >= D) {
+                        const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
+                        m0 = (m0 * fn1) / fn + acc.r / fn;
+                        m1 = (m1 * fn1) / fn + acc.g / fn;
+                        m2 = (m2 * fn1) / fn + acc.b / fn;
+                        ++samples;
+                        if (n >= a.spp) {
+                            float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+                            o3[0] = (float)m0;
+                            o3[1] = (float)m1;
+                            o3[2] = (float)m2;
+                            state = ST_IDLE;
+                            break;
+                        }
+                        ++n;
+                        if (start_sample()) again = true;
+                        break;
+                    }
+                    if (skip_dead && czero(wgt)) {       // dead path: replay the draws only
+                        ++reference;
+                        const float u = rng_uniform(rng);
+                        if (u < 0.5) { rng_next(rng); rng_next(rng); }
+                        else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
+                        ++i;
+                        continue;
+                    }
+                    ++reference;
+                    if (begin_trace(ro, rd)) again = true;
+                    break;
+                }
+            }
+        }
+    }
+    const unsigned long long c0 = wave_sum(traced), c1 = wave_sum(reference), c4 = wave_sum(samples);
+    unsigned long long c2 = 0, c3v = 0;
+    if (kCount) { c2 = wave_sum(cnt.nodes); c3v = wave_sum(cnt.tris); }
+    if (lane == 0) {
+        atomicAdd(a.counters + 0, c0);
+        atomicAdd(a.counters + 1, c1);
+        atomicAdd(a.counters + 4, c4);
+        if (kCount) { atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); }
+    }
+}
+
 // ------------------------------------------------------------------ host side
 #define HIP_TRY(expr)                                                                            \
     do {                                                                                         \
@@ -507,6 +732,11 @@ struct pt_ctx {
     float scene_extent = 1.0f;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cus = 256;
+    uint32_t* pixel_counter = nullptr;
+    bool scene_fast = false;
+    uint32_t node_mask = 0;
+    uint32_t wf_threshold = 24;
+    uint32_t wf_waves_per_cu = 16;
 };
 
 extern "C" {
@@ -626,6 +856,24 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         }
         c->scene_extent = (ext > 0.0f && std::isfinite(ext)) ? ext : 1.0f;
     }
+    {
+        // Markstein-quotient precondition on the scene (pt_device.h div_mk): every vertex
+        // coordinate is 0 or has magnitude in [2^-50, 2^20].  Boxes are min/max of vertices.
+        bool ok = true;
+        for (uint32_t v = 0; v < sc->num_verts && ok; ++v) {
+            const float q[3] = {sc->verts[v].x, sc->verts[v].y, sc->verts[v].z};
+            for (int k = 0; k < 3; ++k) {
+                const float m = std::fabs(q[k]);
+                if (!(m == 0.0f || (m >= 0x1p-50f && m <= 0x1p20f))) ok = false;
+            }
+        }
+        c->scene_fast = ok;
+        uint32_t bits = 1;
+        while ((1u << bits) < nn) ++bits;
+        c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
+        if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
+    }
     std::vector<DShade> sh(nt);
     for (uint32_t i = 0; i < nt; ++i) {
         sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
@@ -668,6 +916,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     }
     if (hipMalloc(reinterpret_cast<void**>(&c->counters), 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), 16) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         pt_destroy(c);
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
@@ -681,7 +930,7 @@ void pt_destroy(pt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
-                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out};
+                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -730,13 +979,31 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const size_t lds = (size_t)a.stack_words * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
 
+    a.pixel_counter = c->pixel_counter;
+    a.nunits = a.ntiles_shard * 64u;
+    a.scene_fast = c->scene_fast ? 1u : 0u;
+    a.wf_threshold = c->wf_threshold;
+    a.node_mask = c->node_mask;
+    const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk;
     HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
+    HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
     const uint32_t waves_per_cu = 16;
     uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
     if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
     HIP_TRY(hipEventRecord(c->ev0, stream));
-    if (p->spp > 0 && a.ntiles_shard > 0) {
+    if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
+        // 4 waves per block, one packed-stack slab of (depth+2) entries x 64 lanes per wave
+        Args b = a;
+        b.stack_words = levels * 64;
+        const size_t lds_wf = (size_t)b.stack_words * 4 * 4;
+        uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
+        const uint32_t need = (a.nunits + 255) / 256;
+        if (blocks > need) blocks = need;
+        if (count) hipLaunchKernelGGL((render_unidir_wf<true>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else hipLaunchKernelGGL((render_unidir_wf<false>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        HIP_TRY(hipGetLastError());
+    } else if (p->spp > 0 && a.ntiles_shard > 0) {
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
         if (p->integrator == PT_INTEGRATOR_HEAD) {
             if (refwalk) { if (count) PT_LAUNCH(1, true, true); else PT_LAUNCH(1, true, false); }
