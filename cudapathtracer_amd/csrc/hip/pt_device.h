@@ -324,7 +324,7 @@ __device__ __forceinline__ float tri_hit(V3 o, V3 d, const DTri* __restrict__ tr
 
 // Resumable state of the culled near-first walk (trace_culled below, one node per step).
 struct Walk {
-    V3 o, d, y;           // ray, y = RN(1/d)
+    V3 y;                 // y = RN(1/d) of the ray being walked (the ray itself stays with the caller)
     uint32_t node;        // current node record
     int32_t sp;           // LDS stack depth
     float best_t;
@@ -336,7 +336,6 @@ struct Walk {
 template <bool kMk>
 __device__ __forceinline__ bool walk_begin(Walk& w, V3 o, V3 d, const float* root, float cull_abs)
 {
-    w.o = o; w.d = d;
     w.y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     w.node = 0; w.sp = 0;
     w.best_t = kMaxFloat; w.best_slot = 0u; w.best_id = 0xffffffffu;
@@ -346,9 +345,9 @@ __device__ __forceinline__ bool walk_begin(Walk& w, V3 o, V3 d, const float* roo
 
 // One node of the walk.  Returns true while the walk continues.
 template <bool kMk, bool kCount>
-__device__ __forceinline__ bool walk_step(Walk& w, const DNode* __restrict__ nodes, const DTri* __restrict__ tris,
-                                          uint32_t* stack, int lane, float cull_rel, float cull_abs,
-                                          uint32_t node_mask, Counters& cnt)
+__device__ __forceinline__ bool walk_step(Walk& w, V3 o, V3 d, const DNode* __restrict__ nodes,
+                                          const DTri* __restrict__ tris, uint32_t* stack, int lane, float cull_rel,
+                                          float cull_abs, uint32_t node_mask, Counters& cnt)
 {
     const DNode* nd = nodes + w.node;
     const float4 A = nd->a, B = nd->b, C = nd->c;
@@ -359,23 +358,23 @@ __device__ __forceinline__ bool walk_step(Walk& w, const DNode* __restrict__ nod
     if (D.x & kLeaf) {
         const uint32_t slot = D.x ^ kLeaf;
         uint32_t id;
-        const float t = tri_hit<kMk>(w.o, w.d, tris + slot, &id);
+        const float t = tri_hit<kMk>(o, d, tris + slot, &id);
         if (kCount) ++cnt.tris;
         if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
     } else {
-        h0 = slab<kMk>(w.o, w.d, w.y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to) && !(to < -cull_abs) &&
+        h0 = slab<kMk>(o, d, w.y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to) && !(to < -cull_abs) &&
              !(ti > w.best_t * cull_rel);
         t0 = ti;
     }
     if (D.y & kLeaf) {
         const uint32_t slot = D.y ^ kLeaf;
         uint32_t id;
-        const float t = tri_hit<kMk>(w.o, w.d, tris + slot, &id);
+        const float t = tri_hit<kMk>(o, d, tris + slot, &id);
         if (kCount) ++cnt.tris;
         if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
         h0 = h0 && !(t0 > w.best_t * cull_rel);
     } else {
-        h1 = slab<kMk>(w.o, w.d, w.y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to) && !(to < -cull_abs) &&
+        h1 = slab<kMk>(o, d, w.y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to) && !(to < -cull_abs) &&
              !(ti > w.best_t * cull_rel);
         t1 = ti;
     }

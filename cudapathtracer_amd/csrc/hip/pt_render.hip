@@ -443,9 +443,12 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
 // until the slowest ray of the wave is done, which is where the tile kernel loses most time.
 // Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
 enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3 };
+#ifndef PT_WF_MIN_WAVES
+#define PT_WF_MIN_WAVES 4
+#endif
 
 template <bool kCount>
-__global__ __launch_bounds__(256) void render_unidir_wf(Args a)
+__global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
 {
     extern __shared__ uint32_t lds_wf[];
     const int lane = threadIdx.x & 63;
@@ -466,9 +469,8 @@ __global__ __launch_bounds__(256) void render_unidir_wf(Args a)
     Rng rng;
     rng.d = rng.v0 = rng.v1 = rng.v2 = rng.v3 = rng.v4 = 0;
     bool lens = false;
-    bool have = false;
-    uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0, k5 = 0;
-    int32_t mtri = -1;
+    bool have = false;          // primary-hit memo valid (only without lens draws: the camera
+    int32_t mtri = -1;          // ray is then the same bits for every sample of the pixel)
     float mt = kMaxFloat;
     int i = 0;
     C3 acc = c3(0, 0, 0), wgt = c3(1, 1, 1);
@@ -497,13 +499,11 @@ __global__ __launch_bounds__(256) void render_unidir_wf(Args a)
         if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
         camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
         ++reference;
-        if (memo_on && have && k0 == __float_as_uint(ro.x) && k1 == __float_as_uint(ro.y) &&
-            k2 == __float_as_uint(ro.z) && k3 == __float_as_uint(rd.x) && k4 == __float_as_uint(rd.y) &&
-            k5 == __float_as_uint(rd.z)) {
+        if (have) {
             htri = mtri; ht = mt; primary = false;
             return true;
         }
-        primary = true;
+        primary = memo_on && !lens;
         return begin_trace(ro, rd);
     };
 
@@ -550,10 +550,10 @@ __global__ __launch_bounds__(256) void render_unidir_wf(Args a)
             const bool allfast = __ballot(state == ST_TRACE && !wfast) == 0ull;
             if (state == ST_TRACE) {
                 const bool more = allfast
-                    ? walk_step<true, kCount>(w, a.nodes, a.tris_leaf, stack, lane, a.cull_rel, a.cull_abs,
-                                              a.node_mask, cnt)
-                    : walk_step<false, kCount>(w, a.nodes, a.tris_leaf, stack, lane, a.cull_rel, a.cull_abs,
-                                               a.node_mask, cnt);
+                    ? walk_step<true, kCount>(w, ro, rd, a.nodes, a.tris_leaf, stack, lane, a.cull_rel,
+                                              a.cull_abs, a.node_mask, cnt)
+                    : walk_step<false, kCount>(w, ro, rd, a.nodes, a.tris_leaf, stack, lane, a.cull_rel,
+                                               a.cull_abs, a.node_mask, cnt);
                 if (!more) {
                     htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
                     ht = w.best_t;
@@ -567,10 +567,8 @@ __global__ __launch_bounds__(256) void render_unidir_wf(Args a)
             bool again = true;
             while (again) {
                 again = false;
-                if (primary && memo_on) {
+                if (primary) {
                     have = true;
-                    k0 = __float_as_uint(ro.x); k1 = __float_as_uint(ro.y); k2 = __float_as_uint(ro.z);
-                    k3 = __float_as_uint(rd.x); k4 = __float_as_uint(rd.y); k5 = __float_as_uint(rd.z);
                     mtri = htri; mt = ht;
                 }
                 primary = false;
