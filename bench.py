@@ -194,7 +194,10 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_tiles",
                     "kernel_ms": round(kms, 3),
-                    "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"])}
+                    "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"]),
+                    "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
+                    "leaf_step_frac": round(counts["leaf_steps"] / max(counts["node_tests"], 1), 4),
+                    "accel_fallbacks": int(counts["accel_fallbacks"])}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget)

@@ -19,6 +19,7 @@ PT_FLAG_REFERENCE_TRAVERSAL = 0x1
 PT_FLAG_NO_DEAD_PATH_SKIP = 0x2
 PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
+PT_FLAG_REFERENCE_BVH = 0x10
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -59,7 +60,8 @@ class Params(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("seconds", C.c_double), ("kernel_ms", C.c_double), ("samples", C.c_uint64),
                 ("rays_traced", C.c_uint64), ("rays_reference", C.c_uint64), ("rays_nominal", C.c_uint64),
-                ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64)]
+                ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("walk_lane_slots", C.c_uint64),
+                ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -40,7 +40,8 @@ static_assert(sizeof(RNode) == 32, "reference node is 32 B");
 struct alignas(16) DTri {
     float4 a;   // v0.xyz, e1.x
     float4 b;   // e1.yz, e2.xy
-    float4 c;   // e2.z, id (bits), -, -
+    float4 c;   // e2.z, id, rank, parent (bits): rank = position in the reference's left-first DFS
+                //   leaf order (tie-break), parent = the reference BVH node whose child it is
 };
 static_assert(sizeof(DTri) == 48, "triangle record is 48 B");
 
@@ -236,8 +237,9 @@ __device__ __forceinline__ bool slab_ref(V3 o, V3 d, float lx, float ly, float l
 }
 
 struct Counters {
-    uint32_t nodes;   // node records fetched (64 B culled walk, 32 B reference walk)
-    uint32_t tris;    // triangle records tested (48 B)
+    uint32_t nodes;        // node records fetched (64 B culled walk, 32 B reference walk)
+    uint32_t tris;         // triangle records tested (48 B)
+    uint32_t leaf_steps;   // walk steps that tested at least one triangle
 };
 
 // ------------------------------------------------------------------ exact division, cheaply
@@ -327,51 +329,71 @@ struct Walk {
     V3 y;                 // y = RN(1/d) of the ray being walked (the ray itself stays with the caller)
     uint32_t node;        // current node record
     int32_t sp;           // LDS stack depth
+    uint32_t tree;        // 0 = render-path SAH BVH, 1 = the reference BVH (exact fallback)
     float best_t;
-    uint32_t best_slot, best_id;
+    uint32_t best_rank, best_id, best_parent;
+};
+
+// The two node/triangle arrays a walk can run on.
+struct Trees {
+    const DNode* nodes[2];
+    const DTri* tris[2];
+    const float* root[2];
 };
 
 // Start a walk: root box test (the reference tests node 0's own box first).  Returns false
 // when the ray misses the root (walk finished, no hit).
+// best_rank starts at 0 so a tie with the MAX_FLOAT sentinel is never accepted (the reference
+// needs t < closestT = MAX_FLOAT); best_id = ~0 marks "no hit yet".
 template <bool kMk>
 __device__ __forceinline__ bool walk_begin(Walk& w, V3 o, V3 d, const float* root, float cull_abs)
 {
     w.y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     w.node = 0; w.sp = 0;
-    w.best_t = kMaxFloat; w.best_slot = 0u; w.best_id = 0xffffffffu;
+    w.best_t = kMaxFloat; w.best_rank = 0u; w.best_id = 0xffffffffu; w.best_parent = 0u;
     float ti, to;
     return slab<kMk>(o, d, w.y, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) && !(to < -cull_abs);
 }
 
+// Candidate update shared by the walks: minimum of (t, reference DFS rank) over 0 < t.
+__device__ __forceinline__ void take_hit(Walk& w, float t, const DTri* __restrict__ tr, uint32_t id)
+{
+    const uint32_t rank = __float_as_uint(tr->c.z);
+    if (0.0f < t && (t < w.best_t || (t == w.best_t && rank < w.best_rank))) {
+        w.best_t = t; w.best_rank = rank; w.best_id = id; w.best_parent = __float_as_uint(tr->c.w);
+    }
+}
+
 // One node of the walk.  Returns true while the walk continues.
 template <bool kMk, bool kCount>
-__device__ __forceinline__ bool walk_step(Walk& w, V3 o, V3 d, const DNode* __restrict__ nodes,
-                                          const DTri* __restrict__ tris, uint32_t* stack, int lane, float cull_rel,
-                                          float cull_abs, uint32_t node_mask, Counters& cnt)
+__device__ __forceinline__ bool walk_step(Walk& w, V3 o, V3 d, const Trees& T, uint32_t* stack, int lane,
+                                          float cull_rel, float cull_abs, uint32_t node_mask, Counters& cnt)
 {
+    const DNode* nodes = w.tree ? T.nodes[1] : T.nodes[0];
+    const DTri* tris = w.tree ? T.tris[1] : T.tris[0];
     const DNode* nd = nodes + w.node;
     const float4 A = nd->a, B = nd->b, C = nd->c;
     const uint4 D = nd->d;
-    if (kCount) ++cnt.nodes;
+    if (kCount) { ++cnt.nodes; if ((D.x | D.y) & kLeaf) ++cnt.leaf_steps; }
     float ti, to, t0 = 0.0f, t1 = 0.0f;
     bool h0 = false, h1 = false;
     if (D.x & kLeaf) {
-        const uint32_t slot = D.x ^ kLeaf;
+        const DTri* tr = tris + (D.x ^ kLeaf);
         uint32_t id;
-        const float t = tri_hit<kMk>(o, d, tris + slot, &id);
+        const float t = tri_hit<kMk>(o, d, tr, &id);
         if (kCount) ++cnt.tris;
-        if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
+        take_hit(w, t, tr, id);
     } else {
         h0 = slab<kMk>(o, d, w.y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to) && !(to < -cull_abs) &&
              !(ti > w.best_t * cull_rel);
         t0 = ti;
     }
     if (D.y & kLeaf) {
-        const uint32_t slot = D.y ^ kLeaf;
+        const DTri* tr = tris + (D.y ^ kLeaf);
         uint32_t id;
-        const float t = tri_hit<kMk>(o, d, tris + slot, &id);
+        const float t = tri_hit<kMk>(o, d, tr, &id);
         if (kCount) ++cnt.tris;
-        if (0.0f < t && (t < w.best_t || (t == w.best_t && slot < w.best_slot))) { w.best_t = t; w.best_slot = slot; w.best_id = id; }
+        take_hit(w, t, tr, id);
         h0 = h0 && !(t0 > w.best_t * cull_rel);
     } else {
         h1 = slab<kMk>(o, d, w.y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to) && !(to < -cull_abs) &&
@@ -400,6 +422,23 @@ __device__ __forceinline__ bool walk_step(Walk& w, V3 o, V3 d, const DNode* __re
         return true;
     }
     return false;
+}
+
+// Winner check for a walk on the render-path BVH: the reference tests a triangle iff the line
+// passes the slab test of every ancestor of its leaf in the reference BVH.  Slab values are
+// correctly rounded, hence monotone in the box bounds, and every ancestor box contains its
+// descendants, so (with no NaN: fast rays have no zero direction component) the parent's test
+// passing implies all ancestors pass.  Returns true when the current best is a triangle the
+// reference would have tested (or there is no hit).
+template <bool kMk>
+__device__ __forceinline__ bool winner_ok(const Walk& w, V3 o, V3 d, const RNode* __restrict__ rnodes)
+{
+    if (w.best_id == 0xffffffffu) return true;
+    const RNode* p = rnodes + w.best_parent;
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(&p->hi[1]);
+    float ti, to;
+    return slab<kMk>(o, d, w.y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to);
 }
 
 // ------------------------------------------------------------------ traversal results
@@ -465,7 +504,7 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
     // best_slot starts at 0 so a tie with the MAX_FLOAT sentinel is never accepted (the
     // reference needs t < closestT = MAX_FLOAT); best_id = ~0 marks "no hit yet".
     float best_t = kMaxFloat;
-    uint32_t best_slot = 0u;
+    uint32_t best_slot = 0u;   // on the reference tree the leaf slot IS the DFS rank
     uint32_t best_id = 0xffffffffu;
     float ti, to;
     if (!slab_ref(o, d, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) || to < -cull_abs) {

@@ -53,6 +53,10 @@ struct Args {
     uint32_t scene_fast;            // all scene coordinates admit the Markstein quotient
     uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
+    const DNode* acc_nodes;         // render-path SAH BVH (child-pair records)
+    const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
+    float acc_root[6];
+    uint32_t use_accel;             // walk the SAH BVH first (winner checked against the reference)
 };
 
 // ------------------------------------------------------------------ per-lane tracer
@@ -382,6 +386,7 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
     tr.lane = lane;
     tr.cnt.nodes = 0;
     tr.cnt.tris = 0;
+    tr.cnt.leaf_steps = 0;
     tr.traced = 0;
     tr.reference = 0;
     unsigned long long samples = 0;
@@ -459,8 +464,10 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
     Counters cnt;
     cnt.nodes = 0;
     cnt.tris = 0;
+    cnt.leaf_steps = 0;
     uint32_t traced = 0, reference = 0;
     unsigned long long samples = 0;
+    uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
 
     uint32_t state = ST_IDLE;
     uint32_t px = 0, py = 0;
@@ -480,12 +487,23 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
     bool primary = false;     // the pending trace is a camera ray (memo store on completion)
     int32_t htri = -1;
     float ht = kMaxFloat;
-    // begin a trace of (o, d); a root miss resolves immediately (returns true = hit known)
+    Trees T;
+    T.nodes[0] = a.use_accel ? a.acc_nodes : a.nodes;
+    T.tris[0] = a.use_accel ? a.acc_tris : a.tris_leaf;
+    T.root[0] = a.use_accel ? a.acc_root : a.root;
+    T.nodes[1] = a.nodes;
+    T.tris[1] = a.tris_leaf;
+    T.root[1] = a.root;
+    uint32_t fallbacks = 0;
+
+    // begin a trace of (o, d); a root miss resolves immediately (returns true = hit known).
+    // Rays outside the Markstein preconditions walk the reference BVH with IEEE division.
     auto begin_trace = [&](V3 o, V3 d) -> bool {
         ++traced;
         wfast = (a.scene_fast != 0u) && ray_fast(o, d);
-        const bool inside = wfast ? walk_begin<true>(w, o, d, a.root, a.cull_abs)
-                                  : walk_begin<false>(w, o, d, a.root, a.cull_abs);
+        w.tree = wfast ? 0u : 1u;
+        const bool inside = wfast ? walk_begin<true>(w, o, d, T.root[0], a.cull_abs)
+                                  : walk_begin<false>(w, o, d, T.root[1], a.cull_abs);
         if (!inside) { htri = -1; ht = kMaxFloat; return true; }
         state = ST_TRACE;
         return false;
@@ -548,12 +566,21 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
             if (tracing == 0ull) break;
             if ((uint32_t)__popcll(__ballot(state == ST_SHADE || state == ST_IDLE)) >= a.wf_threshold) break;
             const bool allfast = __ballot(state == ST_TRACE && !wfast) == 0ull;
+            if (kCount) ++walk_slots;
             if (state == ST_TRACE) {
-                const bool more = allfast
-                    ? walk_step<true, kCount>(w, ro, rd, a.nodes, a.tris_leaf, stack, lane, a.cull_rel,
-                                              a.cull_abs, a.node_mask, cnt)
-                    : walk_step<false, kCount>(w, ro, rd, a.nodes, a.tris_leaf, stack, lane, a.cull_rel,
-                                               a.cull_abs, a.node_mask, cnt);
+                bool more = allfast
+                    ? walk_step<true, kCount>(w, ro, rd, T, stack, lane, a.cull_rel, a.cull_abs, a.node_mask, cnt)
+                    : walk_step<false, kCount>(w, ro, rd, T, stack, lane, a.cull_rel, a.cull_abs, a.node_mask, cnt);
+                if (!more && w.tree == 0u && a.use_accel) {
+                    // the SAH walk's winner must be a triangle the reference tests; else redo the
+                    // ray on the reference BVH (exact by construction)
+                    const bool ok = allfast ? winner_ok<true>(w, ro, rd, a.rnodes) : winner_ok<false>(w, ro, rd, a.rnodes);
+                    if (!ok) {
+                        ++fallbacks;
+                        w.tree = 1u;
+                        more = walk_begin<false>(w, ro, rd, T.root[1], a.cull_abs);
+                    }
+                }
                 if (!more) {
                     htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
                     ht = w.best_t;
@@ -563,6 +590,7 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
         }
 
         // ---------------------------------------------------------------- shade
+        if (kCount) ++shade_slots;
         if (state == ST_SHADE) {
             bool again = true;
             while (again) {
@@ -642,14 +670,22 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
         }
     }
     const unsigned long long c0 = wave_sum(traced), c1 = wave_sum(reference), c4 = wave_sum(samples);
-    unsigned long long c2 = 0, c3v = 0;
-    if (kCount) { c2 = wave_sum(cnt.nodes); c3v = wave_sum(cnt.tris); }
+    unsigned long long c2 = 0, c3v = 0, c5 = 0, c6 = 0, c7 = 0;
+    if (kCount) {
+        c2 = wave_sum(cnt.nodes); c3v = wave_sum(cnt.tris); c5 = wave_sum(walk_slots);
+        c6 = wave_sum(cnt.leaf_steps); c7 = wave_sum(shade_slots);
+    }
     if (lane == 0) {
         atomicAdd(a.counters + 0, c0);
         atomicAdd(a.counters + 1, c1);
         atomicAdd(a.counters + 4, c4);
-        if (kCount) { atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); }
+        if (kCount) {
+            atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
+            atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
+        }
     }
+    const unsigned long long c8 = wave_sum(fallbacks);
+    if (lane == 0 && c8) atomicAdd(a.counters + 8, c8);
 }
 
 // ------------------------------------------------------------------ host side
@@ -735,6 +771,11 @@ struct pt_ctx {
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 24;
     uint32_t wf_waves_per_cu = 16;
+    DNode* acc_nodes = nullptr;
+    DTri* acc_tris = nullptr;
+    float acc_root[6];
+    int32_t acc_depth = 0;
+    bool have_accel = false;
 };
 
 extern "C" {
@@ -799,6 +840,11 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     c->num_tris = nt;
     c->depth = sc->bvh_depth;
 
+    std::vector<uint32_t> ref_parent(nt, 0u);
+    for (uint32_t i = 0; i < nn; ++i) {
+        if (sc->bvh[i].left & PT_BVH_LEAF_FLAG) ref_parent[sc->bvh[i].left ^ PT_BVH_LEAF_FLAG] = i;
+        if (sc->bvh[i].right & PT_BVH_LEAF_FLAG) ref_parent[sc->bvh[i].right ^ PT_BVH_LEAF_FLAG] = i;
+    }
     auto tri_rec = [&](uint32_t k) {
         const pt_triangle& t = sc->tris[k];
         const pt_vec3 a = sc->verts[t.v0], b = sc->verts[t.v1], cc = sc->verts[t.v2];
@@ -807,10 +853,10 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         const float e2x = cc.x - a.x, e2y = cc.y - a.y, e2z = cc.z - a.z; // modelLoader.h:59
         r.a = make_float4(a.x, a.y, a.z, e1x);
         r.b = make_float4(e1y, e1z, e2x, e2y);
-        uint32_t id = k;
-        float idf;
-        memcpy(&idf, &id, 4);
-        r.c = make_float4(e2z, idf, 0.0f, 0.0f);
+        const uint32_t words[3] = {k, leaf_rank[k], ref_parent[k]};
+        float f[3];
+        memcpy(f, words, sizeof(f));
+        r.c = make_float4(e2z, f[0], f[1], f[2]);
         return r;
     };
     std::vector<DTri> tl(nt), to(nt);
@@ -872,6 +918,28 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
     }
+    // render-path SAH BVH (accel_build.cpp); disabled by PT_NO_ACCEL=1 or when too deep for LDS
+    std::vector<DNode> an;
+    std::vector<DTri> at;
+    {
+        pt::AccelBvh acc;
+        const bool want = !(getenv("PT_NO_ACCEL") && atoi(getenv("PT_NO_ACCEL")) != 0);
+        if (want && pt::build_accel(*sc, &acc) == PT_OK && acc.depth < 60 && acc.nodes.size() == nn) {
+            an.resize(acc.nodes.size());
+            for (size_t i = 0; i < acc.nodes.size(); ++i) {
+                const pt::AccelNode& x = acc.nodes[i];
+                an[i].a = make_float4(x.box[0][0], x.box[0][1], x.box[0][2], x.box[0][3]);
+                an[i].b = make_float4(x.box[0][4], x.box[0][5], x.box[1][0], x.box[1][1]);
+                an[i].c = make_float4(x.box[1][2], x.box[1][3], x.box[1][4], x.box[1][5]);
+                an[i].d = make_uint4(x.child[0], x.child[1], 0u, 0u);
+            }
+            at.resize(nt);
+            for (uint32_t i = 0; i < nt; ++i) at[i] = tri_rec(acc.leaf_order[i]);
+            memcpy(c->acc_root, acc.root_box, sizeof(c->acc_root));
+            c->acc_depth = acc.depth;
+            c->have_accel = true;
+        }
+    }
     std::vector<DShade> sh(nt);
     for (uint32_t i = 0; i < nt; ++i) {
         sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
@@ -908,11 +976,12 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     int rc = PT_OK;
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
-        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump))) {
+        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) ||
+        (c->have_accel && ((rc = upload(&c->acc_nodes, an)) || (rc = upload(&c->acc_tris, at))))) {
         pt_destroy(c);
         return bail(rc);
     }
-    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 8 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), 16) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -928,7 +997,8 @@ void pt_destroy(pt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
-                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter};
+                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
+                    c->acc_nodes, c->acc_tris};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -972,7 +1042,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.cull_abs = c->scene_extent * 1e-4f;
     const bool refwalk = (p->flags & PT_FLAG_REFERENCE_TRAVERSAL) != 0;
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
-    const uint32_t levels = (uint32_t)c->depth + 2;
+    const uint32_t levels = (uint32_t)(c->depth > c->acc_depth ? c->depth : c->acc_depth) + 2;
     a.stack_words = levels * 128;
     const size_t lds = (size_t)a.stack_words * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
@@ -982,8 +1052,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
     a.node_mask = c->node_mask;
+    a.use_accel = (c->have_accel && !(p->flags & PT_FLAG_REFERENCE_BVH)) ? 1u : 0u;
+    a.acc_nodes = c->acc_nodes;
+    a.acc_tris = c->acc_tris;
+    memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk;
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
     const uint32_t waves_per_cu = 16;
@@ -1014,7 +1088,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev1, stream));
-    unsigned long long cnt[8];
+    unsigned long long cnt[16];
     HIP_TRY(hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.0f;
@@ -1027,6 +1101,10 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         st->node_tests = cnt[2];
         st->tri_tests = cnt[3];
         st->samples = cnt[4];
+        st->walk_lane_slots = cnt[5];
+        st->leaf_steps = cnt[6];
+        st->shade_lane_slots = cnt[7];
+        st->accel_fallbacks = cnt[8];
         const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
         st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
     }

@@ -61,6 +61,20 @@ struct HostScene {
 // Deterministic float sin/cos shared with the kernels (defined in hip/pt_render.hip).
 void sincos_det(float theta, float* s, float* c);
 
+// ---- render-path acceleration structure (accel_build.cpp) --------------------------------
+struct AccelNode {
+    float box[2][6];       // child boxes (lo xyz, hi xyz), inflated by `margin`
+    uint32_t child[2];     // inner node index, or PT_BVH_LEAF_FLAG | leaf slot
+};
+struct AccelBvh {
+    std::vector<AccelNode> nodes;        // node 0 = root
+    std::vector<uint32_t> leaf_order;    // triangle id of each leaf slot
+    float root_box[6];
+    int depth = 0;
+    float margin = 0.0f;
+};
+int build_accel(const pt_scene& sc, AccelBvh* out);
+
 // ---- BVH (BVH.h) ------------------------------------------------------------------------
 int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,
               std::vector<pt_bvh_node>* out, int32_t* depth);

@@ -126,6 +126,7 @@ typedef struct pt_ctx pt_ctx;
 #define PT_FLAG_NO_DEAD_PATH_SKIP 0x2u    /* trace every bounce even after the path weight is 0   */
 #define PT_FLAG_NO_PRIMARY_CACHE 0x4u     /* re-trace the (sample-invariant) camera ray per sample  */
 #define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant)     */
+#define PT_FLAG_REFERENCE_BVH 0x10u       /* culled walk on the reference BVH only (no SAH BVH)     */
 
 typedef struct {
     int32_t width, height;   /* image size (IMAGE_WIDTH/HEIGHT, kernel.cu:28-29)                    */
@@ -147,8 +148,14 @@ typedef struct {
                                   samples (differs from rays_traced by the primary-ray cache and
                                   the dead-path skip)                                             */
     uint64_t rays_nominal;     /* W*H*spp*(bounces+1): the kernel.cu:757 formula, in 64-bit       */
-    uint64_t node_tests;       /* box tests (PT_FLAG_COUNT only)                                  */
-    uint64_t tri_tests;        /* triangle tests (PT_FLAG_COUNT only)                             */
+    uint64_t node_tests;       /* node records fetched (PT_FLAG_COUNT only)                       */
+    uint64_t tri_tests;        /* triangle records tested (PT_FLAG_COUNT only)                    */
+    uint64_t walk_lane_slots;  /* PT_FLAG_COUNT, wavefront kernel: 64 x BVH-walk iterations; with
+                                  node_tests gives the SIMD lane utilisation of the walk          */
+    uint64_t leaf_steps;       /* PT_FLAG_COUNT: walk steps that tested a triangle                */
+    uint64_t shade_lane_slots; /* PT_FLAG_COUNT, wavefront kernel: 64 x shading passes            */
+    uint64_t accel_fallbacks;  /* rays re-walked on the reference BVH after the SAH walk's winner
+                                  failed the reference-parent check                              */
 } pt_stats;
 
 /* Upload a scene to HIP device `device` (ordinal among visible devices). */

@@ -54,7 +54,8 @@ def _rmse_tonemapped(a, b):
 
 
 MODES = [0, pt.PT_FLAG_REFERENCE_TRAVERSAL, pt.PT_FLAG_NO_DEAD_PATH_SKIP | pt.PT_FLAG_NO_PRIMARY_CACHE,
-         pt.PT_FLAG_REFERENCE_TRAVERSAL | pt.PT_FLAG_NO_DEAD_PATH_SKIP, pt.PT_FLAG_COUNT]
+         pt.PT_FLAG_REFERENCE_TRAVERSAL | pt.PT_FLAG_NO_DEAD_PATH_SKIP, pt.PT_FLAG_COUNT, pt.PT_FLAG_REFERENCE_BVH,
+         pt.PT_FLAG_REFERENCE_BVH | pt.PT_FLAG_COUNT]
 
 
 @pytest.mark.parametrize("flags", MODES)
@@ -153,7 +154,11 @@ def test_culled_walk_agrees_with_reference_walk_standin(tmp_path):
     w, h = 96, 64
     cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
     with pt.Renderer(s, 0) as r:
-        a, sa = r.render(cam, w, h, 4, bounces=3)
+        a, sa = r.render(cam, w, h, 4, bounces=3, flags=pt.PT_FLAG_COUNT)
         b, sb = r.render(cam, w, h, 4, bounces=3, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
+        c, sc = r.render(cam, w, h, 4, bounces=3, flags=pt.PT_FLAG_REFERENCE_BVH)
     assert _bits_equal(a, b.astype(np.float64)) == 0
-    assert sa["rays_reference"] == sb["rays_reference"]
+    assert _bits_equal(c, b.astype(np.float64)) == 0
+    assert sa["rays_reference"] == sb["rays_reference"] == sc["rays_reference"]
+    # the SAH walk's winners are checked against the reference BVH; re-walks must be rare
+    assert sa["accel_fallbacks"] <= max(10, sa["rays_traced"] // 10000)
