@@ -1,0 +1,145 @@
+"""Host surface (C++ in libptamd.so) vs arrays produced by the REFERENCE's own loadOBJ/buildBVH/
+camera/PPM code (compiled from /root/reference by oracle/refgen; fixtures in tests/golden).
+Bar: byte-identical."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, MODELS, SCENE_SETS, golden, load_scene
+
+import cudapathtracer_amd as pt
+from cudapathtracer_amd import api
+
+
+@pytest.mark.parametrize("name", sorted(SCENE_SETS))
+def test_scene_arrays_match_reference(name):
+    """verts/tris/mats/lights/totalLightArea (modelLoader.h:125-210) and the BVH node array
+    (BVH.h:443-474) are byte-identical to the reference's."""
+    g = golden("scene_%s.npz" % name)
+    s = load_scene(name, build_bvh=False)
+    if len(g["tris"]) >= 2:
+        s.build_bvh()
+    a = s.arrays()
+    for k in ("verts", "tris", "mats", "lights", "bvh"):
+        assert a[k].tobytes() == g[k].tobytes(), k
+    assert np.float32(a["total_light_area"]).tobytes() == np.float32(g["total_light_area"]).tobytes()
+    assert a["bvh_depth"] == int(g["bvh_depth"])
+
+
+def test_standin_262k_matches_reference_hashes(tmp_path):
+    """The ~262K-triangle stand-in: every array's sha256 equals the reference build's."""
+    from cudapathtracer_amd import scenes
+    ref = json.load(open(os.path.join(GOLD, "standin.json")))
+    p = scenes.write_sponza_standin(str(tmp_path))
+    assert hashlib.sha256(open(p, "rb").read()).hexdigest() == ref["obj_sha256"]
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    s.build_bvh()
+    a = s.arrays()
+    for k in ("verts", "tris", "mats", "lights", "bvh"):
+        assert hashlib.sha256(a[k].tobytes()).hexdigest() == ref[k], k
+    assert a["bvh_depth"] == int(ref["meta"][7])
+    assert len(a["tris"]) == int(ref["meta"][1]) == 262782
+
+
+def test_quirks_semantics():
+    """tinyobj 0.9.13 corners: fan triangulation, vt/vn-keyed vertex dedupe, unknown material
+    (-1 -> matsOffset-1), unparseable '.5' -> 0, shape split at usemtl/g/o, first-face material."""
+    s = load_scene("quirks", build_bvh=False)
+    a = s.arrays()
+    v = a["verts"]
+    assert v[0]["x"] == 0 and v[2]["y"] == np.float32(1.0)
+    # 'v .5 1 0.25': x fails to parse -> 0 ; '1.5E-1' parses
+    xs = sorted(set(np.round(v["x"].astype(np.float64), 6)))
+    assert 0.15 in [round(x, 6) for x in xs]
+    # materials pushed twice: 3 from quirks.mtl (matA, matB, glow) -> 6
+    assert len(a["mats"]) == 6
+    # the 'glow' material (Ke 2.5 0 1) makes its triangles lights
+    assert len(a["lights"]) >= 1
+    assert s.warning == ""
+
+
+def test_missing_mtl_stops_reading_like_tinyobj():
+    """A missing .mtl makes tinyobj return at the mtllib line (tiny_obj_loader.cc:794-810):
+    no triangles, one default material (pushed twice), and a warning, not an error."""
+    s = load_scene("nomtl", build_bvh=False)
+    a = s.arrays()
+    assert len(a["tris"]) == 0 and len(a["mats"]) == 2
+    assert "not found" in s.warning
+    with pytest.raises(pt.PtError) as e:
+        s.build_bvh()
+    assert e.value.code == -3     # decision d5: fewer than 2 triangles
+
+
+def test_load_errors():
+    s = pt.Scene()
+    with pytest.raises(pt.PtError) as e:
+        s.load_obj(os.path.join(MODELS, "does_not_exist.obj"), mtl_basepath=MODELS + "/")
+    assert e.value.code == -2
+    bad = os.path.join(GOLD, "..", "bad_index.obj")
+    try:
+        with open(bad, "w") as fh:
+            fh.write("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 9\n")
+        with pytest.raises(pt.PtError):
+            pt.Scene().load_obj(bad, mtl_basepath=MODELS + "/")
+    finally:
+        os.remove(bad)
+
+
+def test_morton_matches_reference():
+    g = golden("kat_morton.npz")
+    xy = g["xy"]
+    for i in list(range(0, 1 << 16, 257)) + [0, 1, 2, 3, 65535]:
+        x, y = pt.morton_i_to_pxl(i)
+        assert (x | (y << 16)) == int(xy[i])
+        assert pt.morton_pxl_to_i(x, y) == int(g["back"][i])
+
+
+def test_camera_ray_matches_reference():
+    """cameraRay (camera.h:77-97).  Radius 0: exact bits with no lens draws (the reference's
+    lens term is +0 for the KAT's draws).  Radius > 0: within 1 ulp (the lens angle goes
+    through the deterministic kernel sin/cos instead of cosf/sinf)."""
+    g = golden("kat_cam.npz")
+    for ci in range(4):
+        c = g["cam%d" % ci]
+        cam = pt.make_camera(tuple(c[:3]), c[3], c[4], c[5], int(c[6]), int(c[7]))
+        for k in range(0, len(g["idx%d" % ci]), 7):
+            u1, u2 = g["u%d" % ci][k]
+            o, d = pt.camera_ray(cam, int(g["idx%d" % ci][k]), lens=c[5] != 0, u1=u1, u2=u2)
+            got = np.array(o + d, dtype=np.float32)
+            ref = g["ray%d" % ci][k]
+            if c[5] == 0:
+                assert got.tobytes() == ref.tobytes(), (ci, k)
+            else:
+                assert np.all(np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32)) <= 2), (ci, k)
+
+
+def test_tonemap_and_ppm_match_reference(tmp_path):
+    """kernel.cu:763-778: tone map (int)(gammaCorrect(normalized(c), 1/2.2)*255) and the PPM
+    text layout (rows top-down, x mirrored, trailing-space separated)."""
+    g = golden("kat_tone.npz")
+    c, v = g["c"], g["v"]
+    for i in range(len(c)):
+        for ch in range(3):
+            assert pt.tonemap_u8(float(c[i, ch])) == int(v[i, ch])
+    w, h = 5, 3
+    img = np.arange(w * h * 3, dtype=np.float64).reshape(h, w, 3) / 7.0
+    p = str(tmp_path / "x.ppm")
+    pt.write_ppm(p, img)
+    txt = open(p).read()
+    assert txt.startswith("P3 5 3 255\n")
+    vals = [int(t) for t in txt.split("\n", 1)[1].split()]
+    exp = []
+    for y in range(h):
+        for x in range(w - 1, -1, -1):
+            exp += [pt.tonemap_u8(img[y, x, k]) for k in range(3)]
+    assert vals == exp
+    pt.write_ppm(str(tmp_path / "y.ppm"), img.astype(np.float32))
+    assert os.path.getsize(str(tmp_path / "y.ppm")) > 0
+
+
+def test_structs_match_reference_layouts():
+    assert api.VEC3.itemsize == 12 and api.TRI.itemsize == 28 and api.MAT.itemsize == 48 and api.NODE.itemsize == 32

@@ -121,8 +121,12 @@ def kat_aabb(tmp, rng):
 
 
 def kat_cam(tmp, rng):
+    # radius-0 cameras: lens angle kept in (0, pi/2) so the reference's lens term r*cos, r*sin is +0
+    # (with cos/sin < 0 it is -0 and only flips the sign of a zero direction component; in the
+    # reference those draws come from the racy state[0], kernel.cu:547).  The last camera has a
+    # real lens (compared within 1 ulp: cosf/sinf vs the deterministic kernel sin/cos).
     cams = [((0.0, 1.0, 3.0), 1.0, 3.0, 0.0, 512, 512), ((0.0, 2.6, 13.2), 1.0, 3.0, 0.0, 1920, 1080),
-            ((0.5, -1.0, 2.0), 2.0, 1.5, 0.0, 97, 61)]
+            ((0.5, -1.0, 2.0), 2.0, 1.5, 0.0, 97, 61), ((0.0, 1.0, 3.0), 1.0, 3.0, 0.05, 64, 64)]
     out = {}
     for ci, (pos, dist, focal, radius, w, h) in enumerate(cams):
         camb = np.zeros(8, dtype=np.float32)
@@ -134,6 +138,8 @@ def kat_cam(tmp, rng):
         xs = rng.integers(0, w, n)
         idx = np.array([scenes_morton(x, y) for x, y in zip(xs, ys)], dtype=np.uint32)
         u = rng.uniform(0, 1, (n, 2)).astype(np.float32)
+        if radius == 0.0:
+            u[:, 1] = rng.uniform(1e-3, 0.24, n).astype(np.float32)
         inb = camb + np.concatenate([idx[:, None].view(np.float32), u], 1).astype(np.float32).tobytes()
         open(os.path.join(tmp, "cam.in"), "wb").write(inb)
         run_ref(["cam", os.path.join(tmp, "cam.in"), os.path.join(tmp, "cam.out")])
