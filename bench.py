@@ -64,11 +64,12 @@ def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
     ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"],
                          width, height)
     ntiles = shard.tiles_shape(width, height)[0] * shard.tiles_shape(width, height)[1]
-    # calibrate on one tile, then size the subset (every k-th tile, full spp) to the budget
+    # calibrate on a spread of tiles, then size the subset (every k-th tile, full spp) to the budget
+    cal_tiles = np.linspace(0, ntiles - 1, 4 * threads).astype(np.int64)
     t0 = time.time()
-    cal_pix = shard.tile_pixels(width, height, np.array([ntiles // 2]))
-    oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=cal_pix, threads=threads)
-    dt = max(time.time() - t0, 1e-3)
+    oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=shard.tile_pixels(width, height, cal_tiles),
+                  threads=threads)
+    dt = max(time.time() - t0, 1e-3) / len(cal_tiles)
     tiles_fit = max(1, int(budget_s / dt))
     stride = max(1, ntiles // tiles_fit)
     tiles = np.arange(stride // 2, ntiles, stride)[:tiles_fit]
@@ -97,7 +98,7 @@ def main():
     ap.add_argument("--integrator", type=int, default=0)
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-count", action="store_true", help="skip the counting pass (roofline bytes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -192,7 +193,7 @@ def main():
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_tiles",
+                    "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_unidir_wf" if args.integrator == 0 and not (args.flags & 1) else "render_tiles",
                     "kernel_ms": round(kms, 3),
                     "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"]),
                     "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
