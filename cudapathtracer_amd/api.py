@@ -190,3 +190,18 @@ class Renderer:
         L.check(L.lib().pt_render_device(self._h, C.byref(p), C.byref(cam), C.c_void_p(int(d_out_ptr)),
                                          None if stream_ptr is None else C.c_void_p(int(stream_ptr)), C.byref(st)))
         return st.as_dict()
+
+    def trace(self, origins, directions, reference_bvh=False):
+        """The reference's trace() (kernel.cu:112-161) for a batch of rays: returns
+        (tri int32[n] original triangle index or -1, t float32[n] closestT, 1e5 on a miss)."""
+        o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
+        if o.shape != d.shape:
+            raise ValueError("origins and directions differ in shape")
+        rays = np.ascontiguousarray(np.concatenate([o, d], axis=1))
+        n = len(rays)
+        tri = np.empty(n, dtype=np.int32)
+        t = np.empty(n, dtype=np.float32)
+        L.check(L.lib().pt_trace(self._h, n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data,
+                                 L.PT_FLAG_REFERENCE_BVH if reference_bvh else 0))
+        return tri, t

@@ -254,7 +254,8 @@ __device__ __forceinline__ float div_mk(float x, float d, float y)
 {
     const float q0 = x * y;
     const float r = __builtin_fmaf(-q0, d, x);
-    return __builtin_fmaf(r, y, q0);
+    // d = +-0: y = +-inf and x*y is exactly x/d (+-inf, or NaN for x = 0)
+    return (d == 0.0f) ? q0 : __builtin_fmaf(r, y, q0);
 }
 
 __device__ __forceinline__ bool coord_ok(float v)
@@ -263,10 +264,15 @@ __device__ __forceinline__ bool coord_ok(float v)
     return a == 0.0f || (a >= 0x1p-50f && a <= 0x1p20f);
 }
 
+__device__ __forceinline__ bool dir_ok(float v)
+{
+    const float a = __builtin_fabsf(v);
+    return a == 0.0f || a >= 0x1p-100f;
+}
+
 __device__ __forceinline__ bool ray_fast(V3 o, V3 d)
 {
-    return coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && __builtin_fabsf(d.x) >= 0x1p-100f &&
-           __builtin_fabsf(d.y) >= 0x1p-100f && __builtin_fabsf(d.z) >= 0x1p-100f;
+    return coord_ok(o.x) && coord_ok(o.y) && coord_ok(o.z) && dir_ok(d.x) && dir_ok(d.y) && dir_ok(d.z);
 }
 
 // slab test of BVH.h:51-83; kMk selects the Markstein quotient (same bits as '/').
@@ -439,6 +445,237 @@ __device__ __forceinline__ bool winner_ok(const Walk& w, V3 o, V3 d, const RNode
     const float4 b = *reinterpret_cast<const float4*>(&p->hi[1]);
     float ti, to;
     return slab<kMk>(o, d, w.y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to);
+}
+
+// ------------------------------------------------------------------ 4-wide render-path walk
+// Node of the render-path BVH4 (collapsed SAH BVH): 4 child boxes SoA + 4 child refs, 128 B.
+struct alignas(16) DNode4 {
+    float4 lox, loy, loz, hix, hiy, hiz;
+    uint4 child;     // inner index, kLeaf | slot, or 0xffffffff (empty)
+    uint4 pad;
+};
+static_assert(sizeof(DNode4) == 128, "BVH4 node is 128 B");
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kRing = 16;                 // LDS stack entries per lane; deeper entries spill to HBM
+
+enum : uint32_t { W4_FILTER = 1u, W4_ZERO_DIR = 2u, W4_FAST = 4u };
+
+struct W4 {
+    V3 inv;              // RN(1/d): also the Markstein reciprocal for the exact checks
+    V3 oi;               // o * inv, for the conservative box test t = fma(b, inv, -oi)
+    uint32_t node;
+    int32_t sp;
+    uint32_t flags;
+    float best_t;
+    uint32_t best_rank, best_id, best_parent;
+};
+
+// The exact reference test a winner must pass (DESIGN.md "Traversal" 2): the reference slab test
+// on its reference parent -- or, when a direction component is 0 (NaN slab values possible),
+// on every ancestor up the reference tree.
+__device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d, uint32_t flags,
+                                           const RNode* __restrict__ rnodes, const uint32_t* __restrict__ rparent)
+{
+    const V3 y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // IEEE reciprocals: div_mk's y
+    uint32_t n = parent;
+    for (;;) {
+        const RNode* p = rnodes + n;
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(&p->hi[1]);
+        float ti, to;
+        if (!slab<true>(o, d, y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to)) return false;
+        if (!(flags & W4_ZERO_DIR) || n == 0u) return true;
+        n = rparent[n];
+    }
+}
+
+// Only rays satisfying ray_fast() walk the BVH4 (all exact tests use Markstein quotients);
+// the others take trace_slow() below.
+__device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root, float cull_abs)
+{
+    // Conservative slab values are lo*inv - o*inv (one FMA).  A zero component would make that
+    // inf - inf = NaN on one plane and -inf on the other, which min/max cannot repair, so the
+    // reciprocal is clamped to +-2^100: o*inv stays finite (|o| <= 2^20), and the inflated boxes
+    // keep every plane >= margin from an origin inside the true slab, so the signs -- hence
+    // "inside: unbounded, outside: rejected" -- come out right.  Exact tests use 1/d itself.
+    w.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (d.x == 0.0f) w.inv.x = __builtin_copysignf(0x1p100f, w.inv.x);
+    if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, w.inv.y);
+    if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, w.inv.z);
+    w.oi = v3(o.x * w.inv.x, o.y * w.inv.y, o.z * w.inv.z);
+    w.node = 0; w.sp = 0;
+    w.flags = W4_FAST | ((d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) ? W4_ZERO_DIR : 0u);
+    w.best_t = kMaxFloat; w.best_rank = 0u; w.best_id = 0xffffffffu; w.best_parent = 0u;
+    // conservative root test (boxes inflated; NaN planes are ignored by min/max)
+    const float x0 = __builtin_fmaf(root[0], w.inv.x, -w.oi.x), x1 = __builtin_fmaf(root[3], w.inv.x, -w.oi.x);
+    const float y0 = __builtin_fmaf(root[1], w.inv.y, -w.oi.y), y1 = __builtin_fmaf(root[4], w.inv.y, -w.oi.y);
+    const float z0 = __builtin_fmaf(root[2], w.inv.z, -w.oi.z), z1 = __builtin_fmaf(root[5], w.inv.z, -w.oi.z);
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)), __builtin_fminf(z0, z1));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)), __builtin_fmaxf(z0, z1));
+    return !(tn > tf) && !(tf < -cull_abs);
+}
+
+// Conservative 4-box test; returns entry distances (+inf = not entered).
+__device__ __forceinline__ float box_enter(const W4& w, float lx, float ly, float lz, float hx, float hy, float hz,
+                                           float limit, float cull_abs)
+{
+    const float x0 = __builtin_fmaf(lx, w.inv.x, -w.oi.x), x1 = __builtin_fmaf(hx, w.inv.x, -w.oi.x);
+    const float y0 = __builtin_fmaf(ly, w.inv.y, -w.oi.y), y1 = __builtin_fmaf(hy, w.inv.y, -w.oi.y);
+    const float z0 = __builtin_fmaf(lz, w.inv.z, -w.oi.z), z1 = __builtin_fmaf(hz, w.inv.z, -w.oi.z);
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)), __builtin_fminf(z0, z1));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)), __builtin_fmaxf(z0, z1));
+    const bool in = !(tn > tf) && !(tf < -cull_abs) && !(tn > limit);
+    return in ? tn : INFINITY;
+}
+
+__device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32_t& rb)
+{
+    const bool s = tb < ta;
+    const float t = s ? tb : ta; tb = s ? ta : tb; ta = t;
+    const uint32_t r = s ? rb : ra; rb = s ? ra : rb; ra = r;
+}
+
+struct Stack4 {
+    uint32_t* ring;       // LDS: entry k of this lane at ring[(k % kRing) * 64 + lane]
+    uint32_t* spill;      // HBM: entry k >= kRing at spill[(k - kRing) * stride]
+    uint32_t stride;
+    int lane;
+};
+
+__device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
+{
+    const int slot = (w.sp % kRing) * 64 + S.lane;
+    if (w.sp >= kRing) S.spill[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
+    S.ring[slot] = e;
+    ++w.sp;
+}
+
+__device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
+{
+    --w.sp;
+    const int slot = (w.sp % kRing) * 64 + S.lane;
+    const uint32_t e = S.ring[slot];
+    if (w.sp >= kRing) S.ring[slot] = S.spill[(size_t)(w.sp - kRing) * S.stride];
+    return e;
+}
+
+// One BVH4 node.  Returns true while the walk continues.
+template <bool kCount>
+__device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
+                                           const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
+                                           float cull_abs, uint32_t node_mask, Counters& cnt)
+{
+    const DNode4* nd = nodes + w.node;
+    const float4 lx = nd->lox, ly = nd->loy, lz = nd->loz, hx = nd->hix, hy = nd->hiy, hz = nd->hiz;
+    const uint4 ch = nd->child;
+    if (kCount) ++cnt.nodes;
+    float lim = w.best_t * cull_rel;
+    float t0 = (ch.x == kEmpty) ? INFINITY : box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
+    float t1 = (ch.y == kEmpty) ? INFINITY : box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
+    float t2 = (ch.z == kEmpty) ? INFINITY : box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
+    float t3 = (ch.w == kEmpty) ? INFINITY : box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
+    uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
+    // leaf children whose (inflated) box is entered: exact triangle test, one at a time
+    uint32_t leaves = ((r0 & kLeaf) && r0 != kEmpty && t0 != INFINITY ? 1u : 0u) |
+                      ((r1 & kLeaf) && r1 != kEmpty && t1 != INFINITY ? 2u : 0u) |
+                      ((r2 & kLeaf) && r2 != kEmpty && t2 != INFINITY ? 4u : 0u) |
+                      ((r3 & kLeaf) && r3 != kEmpty && t3 != INFINITY ? 8u : 0u);
+    while (leaves) {
+        const uint32_t c = __builtin_ctz(leaves);
+        leaves &= leaves - 1u;
+        const uint32_t r = (c == 0u) ? r0 : (c == 1u) ? r1 : (c == 2u) ? r2 : r3;
+        const DTri* tr = tris + (r ^ kLeaf);
+        uint32_t id;
+        const float t = tri_hit<true>(o, d, tr, &id);
+        if (kCount) { ++cnt.tris; if (leaves == 0u) ++cnt.leaf_steps; }
+        const uint32_t rank = __float_as_uint(tr->c.z);
+        if (0.0f < t && (t < w.best_t || (t == w.best_t && rank < w.best_rank))) {
+            w.best_t = t; w.best_rank = rank; w.best_id = id; w.best_parent = __float_as_uint(tr->c.w);
+        }
+    }
+    // inner children, nearest first; entries beyond the (possibly improved) best are dropped
+    lim = w.best_t * cull_rel;
+    if ((r0 & kLeaf) || t0 > lim) t0 = INFINITY;
+    if ((r1 & kLeaf) || t1 > lim) t1 = INFINITY;
+    if ((r2 & kLeaf) || t2 > lim) t2 = INFINITY;
+    if ((r3 & kLeaf) || t3 > lim) t3 = INFINITY;
+    cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
+    if (t3 != INFINITY) push4(w, S, (__float_as_uint(t3) & ~node_mask) | r3);
+    if (t2 != INFINITY) push4(w, S, (__float_as_uint(t2) & ~node_mask) | r2);
+    if (t1 != INFINITY) push4(w, S, (__float_as_uint(t1) & ~node_mask) | r1);
+    if (t0 != INFINITY) { w.node = r0; return true; }
+    while (w.sp > 0) {
+        const uint32_t e = pop4(w, S);
+        if (__uint_as_float(e & ~node_mask) > w.best_t * cull_rel) continue;
+        w.node = e & node_mask;
+        return true;
+    }
+    return false;
+}
+
+// Exact walk for the rare rays the fast path does not take (outside the Markstein
+// preconditions, or a BVH4 winner the reference would not have tested): the culled near-first
+// walk on the reference BVH's child-pair records with IEEE '/' everywhere -- the reference's own
+// slab bits, so every entered box is one the reference enters -- and its stack in HBM
+// (entry k of this lane: node at gs[2k*stride], entry distance at gs[(2k+1)*stride]).
+__device__ __forceinline__ void trace_slow(V3 o, V3 d, const float* root, const DNode* __restrict__ nodes,
+                                        const DTri* __restrict__ tris, uint32_t* gs, uint32_t stride,
+                                        float cull_rel, float cull_abs, int32_t* tri_out, float* t_out)
+{
+    const V3 y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best_t = kMaxFloat;
+    uint32_t best_rank = 0u, best_id = 0xffffffffu;
+    float ti, to;
+    *tri_out = -1;
+    *t_out = kMaxFloat;
+    if (!slab<false>(o, d, y, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) || to < -cull_abs)
+        return;
+    int sp = 0;
+    uint32_t node = 0;
+    for (;;) {
+        const DNode* nd = nodes + node;
+        const float4 A = nd->a, B = nd->b, C = nd->c;
+        const uint4 D = nd->d;
+        bool h0 = false, h1 = false;
+        float t0 = 0.0f, t1 = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t r = c ? D.y : D.x;
+            if (r & kLeaf) {
+                const DTri* tr = tris + (r ^ kLeaf);
+                uint32_t id;
+                const float t = tri_hit<false>(o, d, tr, &id);
+                const uint32_t rank = __float_as_uint(tr->c.z);
+                if (0.0f < t && (t < best_t || (t == best_t && rank < best_rank))) { best_t = t; best_rank = rank; best_id = id; }
+            } else {
+                const bool hit = c ? slab<false>(o, d, y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to)
+                                   : slab<false>(o, d, y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to);
+                const bool in = hit && !(to < -cull_abs) && !(ti > best_t * cull_rel);
+                if (c) { h1 = in; t1 = ti; } else { h0 = in; t0 = ti; }
+            }
+        }
+        h0 = h0 && !(t0 > best_t * cull_rel);
+        if (h0 && h1) {
+            const bool sw = t1 < t0;
+            gs[(size_t)(2 * sp) * stride] = sw ? D.x : D.y;
+            gs[(size_t)(2 * sp + 1) * stride] = __float_as_uint(sw ? t0 : t1);
+            ++sp;
+            node = sw ? D.y : D.x;
+            continue;
+        }
+        if (h0 | h1) { node = h0 ? D.x : D.y; continue; }
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            if (__uint_as_float(gs[(size_t)(2 * sp + 1) * stride]) > best_t * cull_rel) continue;
+            node = gs[(size_t)(2 * sp) * stride];
+            found = true;
+            break;
+        }
+        if (!found) break;
+    }
+    *tri_out = (best_id == 0xffffffffu) ? -1 : (int32_t)best_id;
+    *t_out = best_t;
 }
 
 // ------------------------------------------------------------------ traversal results

@@ -53,10 +53,13 @@ struct Args {
     uint32_t scene_fast;            // all scene coordinates admit the Markstein quotient
     uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
-    const DNode* acc_nodes;         // render-path SAH BVH (child-pair records)
+    const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
+    const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
+    uint32_t* spill;                // LDS-stack overflow, entry k of lane g at spill[(k-kRing)*stride + g]
+    uint32_t spill_stride;
     float acc_root[6];
-    uint32_t use_accel;             // walk the SAH BVH first (winner checked against the reference)
+    uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
 };
 
 // ------------------------------------------------------------------ per-lane tracer
@@ -447,159 +450,160 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
 // direction, finishes samples / pixels and fetches new pixels.  Lanes therefore do not idle
 // until the slowest ray of the wave is done, which is where the tile kernel loses most time.
 // Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
-enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3 };
-#ifndef PT_WF_MIN_WAVES
-#define PT_WF_MIN_WAVES 4
-#endif
+enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4 };
 
-template <bool kCount>
-__global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
+// Per-lane shading state ("cold": not needed while the lane walks) lives in HBM, word k of lane g
+// at cold[k * stride + g] (coalesced), and is loaded/stored only around the shading phase, so the
+// walk phase's register footprint is the ray, the walk state and the stack -- which is what sets
+// the kernel's occupancy.
+enum : int {
+    CW_PX = 0, CW_PY, CW_N, CW_I, CW_FLAGS, CW_MTRI, CW_MT,
+    CW_RNG = 7,                       // d, v0..v4
+    CW_M = 13,                        // m0..m2 (f64, lo/hi words)
+    CW_ACC = 19,                      // acc (f64 x 3)
+    CW_WGT = 25,                      // wgt (f64 x 3)
+    CW_TRACED = 31, CW_REFERENCE, CW_SAMPLES, CW_FALLBACKS,
+    kColdWords = 35
+};
+enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4 };
+
+// Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the word
+// offset k * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
+struct ColdRec {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t voff;      // lane byte offset
+    uint32_t sbytes;    // bytes between consecutive words of one lane
+    __device__ __forceinline__ uint32_t ld(int k) const
+    {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)((uint32_t)k * sbytes), 0);
+    }
+    __device__ __forceinline__ void st(int k, uint32_t v) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32((int)v, rs, (int)voff, (int)((uint32_t)k * sbytes), 0);
+    }
+    __device__ __forceinline__ double ldd(int k) const
+    {
+        return __hiloint2double((int)ld(k + 1), (int)ld(k));
+    }
+    __device__ __forceinline__ void std_(int k, double v) const
+    {
+        st(k, (uint32_t)__double2loint(v));
+        st(k + 1, (uint32_t)__double2hiint(v));
+    }
+};
+
+// kMinWaves: waves per SIMD the register allocation must allow (launch bound); 4 = 128 VGPRs,
+// 5 = 96, 6 = 80 -- more resident waves hide more memory latency, at the price of spilling
+// shading-phase values (the walk loop itself stays spill-free down to 96).
+template <bool kCount, int kMinWaves>
+__global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
     extern __shared__ uint32_t lds_wf[];
     const int lane = threadIdx.x & 63;
-    uint32_t* stack = lds_wf + (threadIdx.x >> 6) * a.stack_words;
     const int D = a.bounces;
-    const bool skip_dead = !(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP);
-    const bool memo_on = !(a.flags & PT_FLAG_NO_PRIMARY_CACHE);
     Counters cnt;
     cnt.nodes = 0;
     cnt.tris = 0;
     cnt.leaf_steps = 0;
-    uint32_t traced = 0, reference = 0;
-    unsigned long long samples = 0;
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
 
+    // hot state: what the walk phase needs
     uint32_t state = ST_IDLE;
-    uint32_t px = 0, py = 0;
-    int n = 0;
-    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-    Rng rng;
-    rng.d = rng.v0 = rng.v1 = rng.v2 = rng.v3 = rng.v4 = 0;
-    bool lens = false;
-    bool have = false;          // primary-hit memo valid (only without lens draws: the camera
-    int32_t mtri = -1;          // ray is then the same bits for every sample of the pixel)
-    float mt = kMaxFloat;
-    int i = 0;
-    C3 acc = c3(0, 0, 0), wgt = c3(1, 1, 1);
     V3 ro = v3(0, 0, 0), rd = v3(0, 0, 1);
-    Walk w;
-    bool wfast = false;
-    bool primary = false;     // the pending trace is a camera ray (memo store on completion)
+    W4 w;
     int32_t htri = -1;
     float ht = kMaxFloat;
-    Trees T;
-    T.nodes[0] = a.use_accel ? a.acc_nodes : a.nodes;
-    T.tris[0] = a.use_accel ? a.acc_tris : a.tris_leaf;
-    T.root[0] = a.use_accel ? a.acc_root : a.root;
-    T.nodes[1] = a.nodes;
-    T.tris[1] = a.tris_leaf;
-    T.root[1] = a.root;
-    uint32_t fallbacks = 0;
-
-    // begin a trace of (o, d); a root miss resolves immediately (returns true = hit known).
-    // Rays outside the Markstein preconditions walk the reference BVH with IEEE division.
-    auto begin_trace = [&](V3 o, V3 d) -> bool {
-        ++traced;
-        wfast = (a.scene_fast != 0u) && ray_fast(o, d);
-        w.tree = wfast ? 0u : 1u;
-        const bool inside = wfast ? walk_begin<true>(w, o, d, T.root[0], a.cull_abs)
-                                  : walk_begin<false>(w, o, d, T.root[1], a.cull_abs);
-        if (!inside) { htri = -1; ht = kMaxFloat; return true; }
-        state = ST_TRACE;
-        return false;
-    };
-    // start sample n of the current pixel: camera ray, then memo or trace; true = hit known
-    auto start_sample = [&]() -> bool {
-        i = 0;
-        acc = c3(0, 0, 0);
-        wgt = c3(1, 1, 1);
-        float u1 = 0.0f, u2 = 0.0f;
-        if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
-        camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
-        ++reference;
-        if (have) {
-            htri = mtri; ht = mt; primary = false;
-            return true;
-        }
-        primary = memo_on && !lens;
-        return begin_trace(ro, rd);
-    };
+    Stack4 S;
+    S.ring = lds_wf + (threadIdx.x >> 6) * a.stack_words;
+    S.lane = lane;
+    S.stride = a.spill_stride;
+    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.spill_stride * 4u), 0x00020000),
+                    (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.spill_stride * 4u};
+    for (int k = 0; k < kColdWords; ++k) R.st(k, 0u);
 
     for (;;) {
-        // ---------------------------------------------------------------- refill
-        const uint64_t idle = __ballot(state == ST_IDLE);
-        if (idle) {
-            const uint32_t need = (uint32_t)__popcll(idle);
-            const int leader = __ffsll((long long)idle) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.pixel_counter, need);
-            base = __shfl(base, leader, 64);
-            if (state == ST_IDLE) {
-                const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                if (u >= a.nunits) {
-                    state = ST_DONE;
-                } else {
-                    const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
-                    const uint32_t l = u & 63u;
-                    const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
-                    const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
-                    px = (t % a.tiles_x) * kTile + qx;
-                    py = (t / a.tiles_x) * kTile + qy;
-                    if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
-                        const uint32_t idx = morton2(px, py);
-                        rng_init(rng, a.seed, idx, a.jump);
-                        lens = (idx == 0) || (a.cam.radius != 0.0f);
-                        have = false;
-                        n = 1;
-                        m0 = m1 = m2 = 0.0;
-                        state = ST_SHADE;      // provisional; start_sample sets TRACE if it traces
-                        if (!start_sample()) state = ST_TRACE;
-                    }
-                }
-            }
-        }
-        if (__ballot(state != ST_DONE) == 0ull) break;
-
         // ---------------------------------------------------------------- walk
         for (;;) {
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
-            if ((uint32_t)__popcll(__ballot(state == ST_SHADE || state == ST_IDLE)) >= a.wf_threshold) break;
-            const bool allfast = __ballot(state == ST_TRACE && !wfast) == 0ull;
+            if ((uint32_t)__popcll(__ballot(state != ST_TRACE && state != ST_DONE)) >= a.wf_threshold) break;
             if (kCount) ++walk_slots;
             if (state == ST_TRACE) {
-                bool more = allfast
-                    ? walk_step<true, kCount>(w, ro, rd, T, stack, lane, a.cull_rel, a.cull_abs, a.node_mask, cnt)
-                    : walk_step<false, kCount>(w, ro, rd, T, stack, lane, a.cull_rel, a.cull_abs, a.node_mask, cnt);
-                if (!more && w.tree == 0u && a.use_accel) {
-                    // the SAH walk's winner must be a triangle the reference tests; else redo the
-                    // ray on the reference BVH (exact by construction)
-                    const bool ok = allfast ? winner_ok<true>(w, ro, rd, a.rnodes) : winner_ok<false>(w, ro, rd, a.rnodes);
-                    if (!ok) {
-                        ++fallbacks;
-                        w.tree = 1u;
-                        more = walk_begin<false>(w, ro, rd, T.root[1], a.cull_abs);
-                    }
-                }
+                const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
+                                                     a.node_mask, cnt);
                 if (!more) {
                     htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
                     ht = w.best_t;
                     state = ST_SHADE;
+                    // the winner must be a triangle the reference tests; if not (rare), the exact
+                    // reference-BVH walk redoes the ray in the shading phase
+                    if (htri >= 0 && !ref_tested(w.best_parent, ro, rd, w.flags, a.rnodes, a.rparent))
+                        state = ST_SLOW;
                 }
             }
         }
 
-        // ---------------------------------------------------------------- shade
+        // ---------------------------------------------------------------- shade + refill
         if (kCount) ++shade_slots;
-        if (state == ST_SHADE) {
-            bool again = true;
+        const bool cold = state != ST_TRACE && state != ST_DONE;
+        if (cold) {
+            uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
+            int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
+            uint32_t fl = R.ld(CW_FLAGS);
+            int32_t mtri = (int32_t)R.ld(CW_MTRI);
+            float mt = __uint_as_float(R.ld(CW_MT));
+            Rng rng;
+            rng.d = R.ld(CW_RNG); rng.v0 = R.ld(CW_RNG + 1); rng.v1 = R.ld(CW_RNG + 2);
+            rng.v2 = R.ld(CW_RNG + 3); rng.v3 = R.ld(CW_RNG + 4); rng.v4 = R.ld(CW_RNG + 5);
+            double m0 = R.ldd(CW_M), m1 = R.ldd(CW_M + 2), m2 = R.ldd(CW_M + 4);
+            C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
+            C3 wgt = c3(R.ldd(CW_WGT), R.ldd(CW_WGT + 2), R.ldd(CW_WGT + 4));
+            uint32_t traced = R.ld(CW_TRACED), reference = R.ld(CW_REFERENCE);
+            uint32_t samples = R.ld(CW_SAMPLES), fallbacks = R.ld(CW_FALLBACKS);
+
+            // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
+            // a ray outside the Markstein preconditions, which takes the exact slow walk)
+            auto begin_trace = [&](V3 o, V3 d) -> bool {
+                ++traced;
+                if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
+                if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
+                    htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
+                }
+                state = ST_TRACE;
+                return false;
+            };
+            // start sample n of the current pixel: camera ray, then memo or trace
+            auto start_sample = [&]() -> bool {
+                i = 0;
+                acc = c3(0, 0, 0);
+                wgt = c3(1, 1, 1);
+                float u1 = 0.0f, u2 = 0.0f;
+                const bool lens = (fl & CF_LENS) != 0u;
+                if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
+                camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
+                ++reference;
+                if (fl & CF_HAVE) {
+                    htri = mtri; ht = mt; fl &= ~CF_PRIMARY; state = ST_SHADE;
+                    return true;
+                }
+                fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
+                return begin_trace(ro, rd);
+            };
+
+            bool again = (state == ST_SHADE || state == ST_SLOW);
             while (again) {
                 again = false;
-                if (primary) {
-                    have = true;
+                if (state == ST_SLOW) {
+                    ++fallbacks;
+                    trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
+                               &htri, &ht);
+                }
+                state = ST_SHADE;
+                if (fl & CF_PRIMARY) {
+                    fl = (fl | CF_HAVE) & ~CF_PRIMARY;
                     mtri = htri; mt = ht;
                 }
-                primary = false;
                 // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
                 {
                     int32_t tri = htri;
@@ -651,10 +655,10 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
                             break;
                         }
                         ++n;
-                        if (start_sample()) again = true;
+                        again = start_sample();
                         break;
                     }
-                    if (skip_dead && czero(wgt)) {       // dead path: replay the draws only
+                    if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
                         ++reference;
                         const float u = rng_uniform(rng);
                         if (u < 0.5) { rng_next(rng); rng_next(rng); }
@@ -663,13 +667,56 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
                         continue;
                     }
                     ++reference;
-                    if (begin_trace(ro, rd)) again = true;
+                    again = begin_trace(ro, rd);
                     break;
                 }
             }
+
+            // refill: lanes whose pixel is finished take the next pixels of this shard
+            const uint64_t idle = __ballot(state == ST_IDLE);
+            if (idle) {
+                const uint32_t need = (uint32_t)__popcll(idle);
+                const int leader = __ffsll((long long)idle) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(a.pixel_counter, need);
+                base = __shfl(base, leader, 64);
+                if (state == ST_IDLE) {
+                    const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                    if (u >= a.nunits) {
+                        state = ST_DONE;
+                    } else {
+                        const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
+                        const uint32_t l = u & 63u;
+                        const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
+                        const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
+                        px = (t % a.tiles_x) * kTile + qx;
+                        py = (t / a.tiles_x) * kTile + qy;
+                        if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
+                            const uint32_t idx = morton2(px, py);
+                            rng_init(rng, a.seed, idx, a.jump);
+                            fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
+                            n = 1;
+                            m0 = m1 = m2 = 0.0;
+                            start_sample();
+                        }
+                    }
+                }
+            }
+
+            R.st(CW_PX, px); R.st(CW_PY, py); R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i);
+            R.st(CW_FLAGS, fl); R.st(CW_MTRI, (uint32_t)mtri); R.st(CW_MT, __float_as_uint(mt));
+            R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
+            R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
+            R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
+            R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
+            R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
+            R.st(CW_TRACED, traced); R.st(CW_REFERENCE, reference);
+            R.st(CW_SAMPLES, samples); R.st(CW_FALLBACKS, fallbacks);
         }
+        if (__ballot(state != ST_DONE) == 0ull) break;
     }
-    const unsigned long long c0 = wave_sum(traced), c1 = wave_sum(reference), c4 = wave_sum(samples);
+    const unsigned long long c0 = wave_sum(R.ld(CW_TRACED)), c1 = wave_sum(R.ld(CW_REFERENCE));
+    const unsigned long long c4 = wave_sum(R.ld(CW_SAMPLES)), c8 = wave_sum(R.ld(CW_FALLBACKS));
     unsigned long long c2 = 0, c3v = 0, c5 = 0, c6 = 0, c7 = 0;
     if (kCount) {
         c2 = wave_sum(cnt.nodes); c3v = wave_sum(cnt.tris); c5 = wave_sum(walk_slots);
@@ -679,13 +726,58 @@ __global__ __launch_bounds__(256, PT_WF_MIN_WAVES) void render_unidir_wf(Args a)
         atomicAdd(a.counters + 0, c0);
         atomicAdd(a.counters + 1, c1);
         atomicAdd(a.counters + 4, c4);
+        if (c8) atomicAdd(a.counters + 8, c8);
         if (kCount) {
             atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
             atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
         }
     }
-    const unsigned long long c8 = wave_sum(fallbacks);
-    if (lane == 0 && c8) atomicAdd(a.counters + 8, c8);
+}
+
+// ------------------------------------------------------------------ batched trace()
+// pt_trace: the reference's trace() (kernel.cu:112-161) for a batch of rays, one lane per ray,
+// on the same walk the wavefront kernel uses (BVH4 + winner check + exact slow path), or on the
+// reference BVH with the reference's own stack walk (kRef).
+template <bool kRef>
+__global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restrict__ rays, uint32_t n,
+                                                  int32_t* __restrict__ tri_out, float* __restrict__ t_out)
+{
+    extern __shared__ uint32_t lds_tr[];
+    const int lane = threadIdx.x & 63;
+    Counters cnt;
+    cnt.nodes = cnt.tris = cnt.leaf_steps = 0;
+    Stack4 S;
+    S.ring = lds_tr + (threadIdx.x >> 6) * a.stack_words;
+    S.lane = lane;
+    S.stride = a.spill_stride;
+    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        const V3 o = v3(rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]);
+        const V3 d = v3(rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]);
+        int32_t htri = -1;
+        float ht = kMaxFloat;
+        if (kRef) {
+            const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, S.ring, lane, cnt);
+            htri = h.tri; ht = h.t;
+        } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
+            trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs, &htri, &ht);
+        } else {
+            W4 w;
+            if (walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
+                while (walk4_step<false>(w, o, d, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs, a.node_mask, cnt)) {
+                }
+                htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
+                ht = w.best_t;
+                if (htri >= 0 && !ref_tested(w.best_parent, o, d, w.flags, a.rnodes, a.rparent)) {
+                    atomicAdd(a.counters + 8, 1ull);
+                    trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
+                               &htri, &ht);
+                }
+            }
+        }
+        tri_out[r] = htri;
+        t_out[r] = ht;
+    }
 }
 
 // ------------------------------------------------------------------ host side
@@ -771,12 +863,21 @@ struct pt_ctx {
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 24;
     uint32_t wf_waves_per_cu = 16;
-    DNode* acc_nodes = nullptr;
+    int wf_min_waves = 4;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
+    DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
+    uint32_t* rparent = nullptr;
+    uint32_t* spill = nullptr;
+    size_t spill_words = 0;
     float acc_root[6];
-    int32_t acc_depth = 0;
-    bool have_accel = false;
+    int32_t acc4_depth = 0;
+    uint32_t node4_mask = 0;
 };
+
+// Per-lane HBM words the walks may need: the BVH4 ring's overflow (at most 3 pushes per level)
+// and trace_slow's full stack on the reference BVH.
+static size_t stack_words_per_lane(const pt_ctx* c);
+static int ensure_spill(pt_ctx* c, size_t words);
 
 extern "C" {
 
@@ -916,29 +1017,46 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         while ((1u << bits) < nn) ++bits;
         c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_WF_MIN_WAVES")) {
+            const int v = atoi(e);
+            c->wf_min_waves = (v == 5 || v == 6) ? v : 4;
+        }
+        c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
     }
-    // render-path SAH BVH (accel_build.cpp); disabled by PT_NO_ACCEL=1 or when too deep for LDS
-    std::vector<DNode> an;
+    // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
+    std::vector<DNode4> an;
     std::vector<DTri> at;
     {
         pt::AccelBvh acc;
-        const bool want = !(getenv("PT_NO_ACCEL") && atoi(getenv("PT_NO_ACCEL")) != 0);
-        if (want && pt::build_accel(*sc, &acc) == PT_OK && acc.depth < 60 && acc.nodes.size() == nn) {
-            an.resize(acc.nodes.size());
-            for (size_t i = 0; i < acc.nodes.size(); ++i) {
-                const pt::AccelNode& x = acc.nodes[i];
-                an[i].a = make_float4(x.box[0][0], x.box[0][1], x.box[0][2], x.box[0][3]);
-                an[i].b = make_float4(x.box[0][4], x.box[0][5], x.box[1][0], x.box[1][1]);
-                an[i].c = make_float4(x.box[1][2], x.box[1][3], x.box[1][4], x.box[1][5]);
-                an[i].d = make_uint4(x.child[0], x.child[1], 0u, 0u);
-            }
-            at.resize(nt);
-            for (uint32_t i = 0; i < nt; ++i) at[i] = tri_rec(acc.leaf_order[i]);
-            memcpy(c->acc_root, acc.root_box, sizeof(c->acc_root));
-            c->acc_depth = acc.depth;
-            c->have_accel = true;
+        pt::Accel4 acc4;
+        int rc4 = pt::build_accel(*sc, &acc);
+        if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
+        if (rc4 != PT_OK) { delete c; return bail(rc4); }
+        an.resize(acc4.nodes.size());
+        for (size_t i = 0; i < acc4.nodes.size(); ++i) {
+            const pt::Accel4Node& x = acc4.nodes[i];
+            an[i].lox = make_float4(x.lo[0][0], x.lo[0][1], x.lo[0][2], x.lo[0][3]);
+            an[i].loy = make_float4(x.lo[1][0], x.lo[1][1], x.lo[1][2], x.lo[1][3]);
+            an[i].loz = make_float4(x.lo[2][0], x.lo[2][1], x.lo[2][2], x.lo[2][3]);
+            an[i].hix = make_float4(x.hi[0][0], x.hi[0][1], x.hi[0][2], x.hi[0][3]);
+            an[i].hiy = make_float4(x.hi[1][0], x.hi[1][1], x.hi[1][2], x.hi[1][3]);
+            an[i].hiz = make_float4(x.hi[2][0], x.hi[2][1], x.hi[2][2], x.hi[2][3]);
+            an[i].child = make_uint4(x.child[0], x.child[1], x.child[2], x.child[3]);
+            an[i].pad = make_uint4(0u, 0u, 0u, 0u);
         }
+        at.resize(nt);
+        for (uint32_t i = 0; i < nt; ++i) at[i] = tri_rec(acc.leaf_order[i]);
+        memcpy(c->acc_root, acc.root_box, sizeof(c->acc_root));
+        c->acc4_depth = acc4.depth;
+        uint32_t bits = 1;
+        while ((1u << bits) < (uint32_t)an.size()) ++bits;
+        c->node4_mask = (1u << bits) - 1u;
+    }
+    std::vector<uint32_t> rpar(nn, 0u);
+    for (uint32_t i = 0; i < nn; ++i) {
+        if (!(sc->bvh[i].left & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].left] = i;
+        if (!(sc->bvh[i].right & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].right] = i;
     }
     std::vector<DShade> sh(nt);
     for (uint32_t i = 0; i < nt; ++i) {
@@ -977,7 +1095,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) ||
-        (c->have_accel && ((rc = upload(&c->acc_nodes, an)) || (rc = upload(&c->acc_tris, at))))) {
+        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar))) {
         pt_destroy(c);
         return bail(rc);
     }
@@ -998,7 +1116,7 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->acc_nodes, c->acc_tris};
+                    c->nodes4, c->acc_tris, c->rparent, c->spill};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1042,7 +1160,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.cull_abs = c->scene_extent * 1e-4f;
     const bool refwalk = (p->flags & PT_FLAG_REFERENCE_TRAVERSAL) != 0;
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
-    const uint32_t levels = (uint32_t)(c->depth > c->acc_depth ? c->depth : c->acc_depth) + 2;
+    const uint32_t levels = (uint32_t)c->depth + 2;
     a.stack_words = levels * 128;
     const size_t lds = (size_t)a.stack_words * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
@@ -1052,11 +1170,15 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
     a.node_mask = c->node_mask;
-    a.use_accel = (c->have_accel && !(p->flags & PT_FLAG_REFERENCE_BVH)) ? 1u : 0u;
-    a.acc_nodes = c->acc_nodes;
+    a.nodes4 = c->nodes4;
     a.acc_tris = c->acc_tris;
+    a.rparent = c->rparent;
     memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
-    const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk;
+    // the render-path BVH's box margin assumes ray origins within ~2^6 of the scene extent
+    const float cam_ext = std::fmax(std::fabs(cam->pos.x), std::fmax(std::fabs(cam->pos.y), std::fabs(cam->pos.z)));
+    const bool near_cam = cam_ext <= 64.0f * c->scene_extent;
+    const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
+                           !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam;
     HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
@@ -1065,15 +1187,24 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
     HIP_TRY(hipEventRecord(c->ev0, stream));
     if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
-        // 4 waves per block, one packed-stack slab of (depth+2) entries x 64 lanes per wave
+        // 4 waves per block; per wave an LDS ring of kRing packed entries x 64 lanes, deeper
+        // entries spill to HBM (a BVH4 walk pushes at most 3 entries per level)
         Args b = a;
-        b.stack_words = levels * 64;
+        b.stack_words = kRing * 64;
+        b.node_mask = c->node4_mask;
         const size_t lds_wf = (size_t)b.stack_words * 4 * 4;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         const uint32_t need = (a.nunits + 255) / 256;
         if (blocks > need) blocks = need;
-        if (count) hipLaunchKernelGGL((render_unidir_wf<true>), dim3(blocks), dim3(256), lds_wf, stream, b);
-        else hipLaunchKernelGGL((render_unidir_wf<false>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        const size_t per_lane = stack_words_per_lane(c);
+        if (int rc = ensure_spill(c, (per_lane + kColdWords) * (size_t)blocks * 256)) return rc;
+        b.spill = c->spill;
+        b.spill_stride = blocks * 256;
+        b.cold = c->spill + per_lane * (size_t)b.spill_stride;
+        if (count) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
@@ -1132,3 +1263,77 @@ int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rg
 }
 
 }  // extern "C"
+
+static size_t stack_words_per_lane(const pt_ctx* c)
+{
+    size_t per_lane = (size_t)(3 * c->acc4_depth + 4);
+    if (per_lane < (size_t)(2 * (c->depth + 2))) per_lane = (size_t)(2 * (c->depth + 2));
+    return per_lane;
+}
+
+static int ensure_spill(pt_ctx* c, size_t words)
+{
+    if (c->spill_words >= words) return PT_OK;
+    if (c->spill) (void)hipFree(c->spill);
+    c->spill = nullptr;
+    c->spill_words = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->spill), words * 4));
+    c->spill_words = words;
+    return PT_OK;
+}
+
+extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags)
+{
+    pt::clear_error();
+    if (!c) return pt::fail(PT_E_INVALID, "pt_trace: null context");
+    if (n == 0) return PT_OK;
+    if (!rays || !tri_out || !t_out) return pt::fail(PT_E_INVALID, "pt_trace: null buffer");
+    HIP_TRY(hipSetDevice(c->device));
+    Args a;
+    memset(&a, 0, sizeof(a));
+    a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
+    a.counters = c->counters;
+    memcpy(a.root, c->root, sizeof(a.root));
+    memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
+    a.cull_rel = 1.0f + 1.0f / 1024.0f;
+    a.cull_abs = c->scene_extent * 1e-4f;
+    a.scene_fast = c->scene_fast ? 1u : 0u;
+    a.node_mask = c->node4_mask;
+    a.nodes4 = c->nodes4;
+    a.acc_tris = c->acc_tris;
+    a.rparent = c->rparent;
+    const uint32_t ring = (uint32_t)(c->depth + 2) > (uint32_t)kRing ? (uint32_t)(c->depth + 2) : (uint32_t)kRing;
+    a.stack_words = ring * 64;
+    const size_t lds = (size_t)a.stack_words * 4 * 4;
+    if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_trace: BVH depth %d too deep for the LDS stack", c->depth);
+    uint32_t blocks = (n + 255) / 256;
+    const uint32_t cap = (uint32_t)c->num_cus * 8u;
+    if (blocks > cap) blocks = cap;
+    if (int rc = ensure_spill(c, stack_words_per_lane(c) * (size_t)blocks * 256)) return rc;
+    a.spill = c->spill;
+    a.spill_stride = blocks * 256;
+    float* d_rays = nullptr;
+    int32_t* d_tri = nullptr;
+    float* d_t = nullptr;
+    int rc = PT_OK;
+    auto run = [&]() -> int {
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_rays), (size_t)n * 24));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_tri), (size_t)n * 4));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_t), (size_t)n * 4));
+        HIP_TRY(hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(c->counters, 0, 16 * sizeof(unsigned long long)));
+        if (flags & PT_FLAG_REFERENCE_BVH)
+            hipLaunchKernelGGL((trace_rays<true>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        else
+            hipLaunchKernelGGL((trace_rays<false>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpy(tri_out, d_tri, (size_t)n * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(t_out, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return PT_OK;
+    };
+    rc = run();
+    if (d_rays) (void)hipFree(d_rays);
+    if (d_tri) (void)hipFree(d_tri);
+    if (d_t) (void)hipFree(d_t);
+    return rc;
+}

@@ -176,4 +176,76 @@ int build_accel(const pt_scene& sc, AccelBvh* out)
     return PT_OK;
 }
 
+namespace {
+
+float area_of(const float* b)
+{
+    return surface(b, b + 3);
+}
+
+struct Collapser {
+    const AccelBvh& bin;
+    Accel4& out;
+    int max_depth = 0;
+
+    // Collapse the subtree whose binary root is inner node `b`; returns its 4-wide index.
+    uint32_t run(uint32_t b, int depth)
+    {
+        max_depth = std::max(max_depth, depth);
+        struct Cand { uint32_t ref; float box[6]; };
+        Cand c[4];
+        int n = 2;
+        for (int k = 0; k < 2; ++k) {
+            c[k].ref = bin.nodes[b].child[k];
+            memcpy(c[k].box, bin.nodes[b].box[k], sizeof(c[k].box));
+        }
+        while (n < 4) {   // expand the inner candidate with the largest surface area
+            int pick = -1;
+            float best = -1.0f;
+            for (int k = 0; k < n; ++k) {
+                if (c[k].ref & PT_BVH_LEAF_FLAG) continue;
+                const float a = area_of(c[k].box);
+                if (a > best) { best = a; pick = k; }
+            }
+            if (pick < 0) break;
+            const AccelNode& x = bin.nodes[c[pick].ref];
+            Cand second;
+            second.ref = x.child[1];
+            memcpy(second.box, x.box[1], sizeof(second.box));
+            c[pick].ref = x.child[0];
+            memcpy(c[pick].box, x.box[0], sizeof(c[pick].box));
+            c[n++] = second;
+        }
+        const uint32_t me = static_cast<uint32_t>(out.nodes.size());
+        out.nodes.emplace_back();
+        uint32_t refs[4];
+        for (int k = 0; k < 4; ++k) {
+            if (k >= n) { refs[k] = kAccel4Empty; continue; }
+            refs[k] = (c[k].ref & PT_BVH_LEAF_FLAG) ? c[k].ref : run(c[k].ref, depth + 1);
+        }
+        Accel4Node& nd = out.nodes[me];
+        for (int k = 0; k < 4; ++k) {
+            for (int ax = 0; ax < 3; ++ax) {
+                nd.lo[ax][k] = (k < n) ? c[k].box[ax] : INFINITY;
+                nd.hi[ax][k] = (k < n) ? c[k].box[3 + ax] : -INFINITY;
+            }
+            nd.child[k] = refs[k];
+        }
+        return me;
+    }
+};
+
+}  // namespace
+
+int collapse_accel4(const AccelBvh& bin, Accel4* out)
+{
+    out->nodes.clear();
+    out->nodes.reserve(bin.nodes.size() / 2 + 1);
+    Collapser col{bin, *out};
+    const uint32_t root = col.run(0, 0);
+    if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
+    out->depth = col.max_depth;
+    return PT_OK;
+}
+
 }  // namespace pt

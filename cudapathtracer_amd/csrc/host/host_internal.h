@@ -75,6 +75,19 @@ struct AccelBvh {
 };
 int build_accel(const pt_scene& sc, AccelBvh* out);
 
+// 4-wide collapse of the binary SAH BVH: each node holds up to 4 children (largest-area
+// expansion), empty slots are kAccel4Empty; leaves stay single triangles (same leaf slots).
+constexpr uint32_t kAccel4Empty = 0xffffffffu;
+struct Accel4Node {
+    float lo[3][4], hi[3][4];   // [axis][child]
+    uint32_t child[4];          // inner node index, PT_BVH_LEAF_FLAG | slot, or kAccel4Empty
+};
+struct Accel4 {
+    std::vector<Accel4Node> nodes;       // node 0 = root
+    int depth = 0;
+};
+int collapse_accel4(const AccelBvh& bin, Accel4* out);
+
 // ---- BVH (BVH.h) ------------------------------------------------------------------------
 int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,
               std::vector<pt_bvh_node>* out, int32_t* depth);

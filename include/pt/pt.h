@@ -171,6 +171,12 @@ int pt_render(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float*
 int pt_render_device(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float* d_out,
                      void* stream, pt_stats* stats);
 
+/* The reference's trace() (kernel.cu:112-161) for n rays given as rays[6n] = {o.xyz, d.xyz}
+ * (host buffers): tri_out[i] = winning ORIGINAL triangle index or -1, t_out[i] = its closestT
+ * (MAX_FLOAT = 1e5 on a miss).  flags: 0 = the render path's walk, PT_FLAG_REFERENCE_BVH = the
+ * reference's own stack walk on its BVH.  Bit-identical to the reference for both.  Blocking. */
+int pt_trace(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags);
+
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(void);
 int pt_abi_version(void);

@@ -65,6 +65,8 @@ def lib():
         h.or_uniform.argtypes = [C.POINTER(OXorwow)]
         h.or_uniform.restype = C.c_float
         h.or_sincos.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        h.or_trace_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        h.or_trace_batch.restype = C.c_int
         h.or_tri_intersect.argtypes = [OVec3, OVec3, C.c_void_p, C.c_void_p]
         h.or_tri_intersect.restype = C.c_float
         h.or_ray_aabb.argtypes = [OVec3, OVec3, OVec3, OVec3]
@@ -132,6 +134,19 @@ def trace(scene: OracleScene, o, d):
     if rc != 0:
         raise RuntimeError("stack overflow")
     return tri.value, t.value
+
+
+def trace_batch(scene: OracleScene, origins, directions):
+    """or_trace over many rays (OpenMP): returns (tri int32[n], t float32[n])."""
+    o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
+    rays = np.ascontiguousarray(np.concatenate([o, d], axis=1))
+    n = len(rays)
+    tri = np.empty(n, dtype=np.int32)
+    t = np.empty(n, dtype=np.float32)
+    if lib().or_trace_batch(C.byref(scene.c), n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data) != 0:
+        raise RuntimeError("stack overflow")
+    return tri, t
 
 
 def xorwow_stream(seed, subsequence, n):

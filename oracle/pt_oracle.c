@@ -326,6 +326,20 @@ int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float
     return 0;
 }
 
+int or_trace_batch(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t)
+{
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : bad)
+    for (long r = 0; r < (long)n; ++r) {
+        or_counters cnt;
+        memset(&cnt, 0, sizeof(cnt));
+        const float* q = rays + 6 * r;
+        or_vec3 o = {q[0], q[1], q[2]}, d = {q[3], q[4], q[5]};
+        bad += or_trace(sc, o, d, tri + r, t + r, &cnt) != 0;
+    }
+    return bad;
+}
+
 /* ------------------------------------------------------- sampling helpers */
 static or_vec3 get_tangent(or_vec3 n)                                  /* kernel.cu:44-54 */
 {

@@ -81,6 +81,8 @@ void     or_camera_ray(const or_camera* cam, uint32_t idx, float u1, float u2, o
 
 /* ---- traversal (kernel.cu:112-161); returns 0, or -1 on stack overflow */
 int      or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri, float* t, or_counters* cnt);
+/* or_trace over rays[6n] = {o.xyz, d.xyz} (OpenMP); returns the number of stack overflows. */
+int      or_trace_batch(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t);
 
 /* ---- integrators */
 /* kernel.cu:417-515 radianceAlongSingleStep2 (integrator 0) */
