@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+NODE_BYTES = 128          # one BVH4 node record (6 x float4 child boxes + uint4 children + pad)
+ACCEL_TAG = "bvh4-hbmstate-v1"   # profiles/traffic.json is used only when it was measured on this kernel
 
 
 def log(*a):
@@ -177,17 +179,18 @@ def main():
         kms = float(np.mean(kernel_ms))
         roof = None
         if counts is not None:
-            # algorithmic bytes per launch: 64-B node records fetched + 48-B triangle records tested
-            # + per traced ray 16 B shading record + 48 B material + 12 B/pixel output
+            # algorithmic bytes per launch: 128-B BVH4 node records visited + 48-B triangle records
+            # tested + per traced ray 16 B hit-shading record + 48 B material + 12 B/pixel output
             npx = counts["samples"] / max(args.spp, 1)
-            bytes_launch = (counts["node_tests"] * 64 + counts["tri_tests"] * 48 +
+            bytes_launch = (counts["node_tests"] * NODE_BYTES + counts["tri_tests"] * 48 +
                             counts["rays_traced"] * (16 + 48) + npx * 12)
             achieved = bytes_launch / (kms * 1e-3) / 1e9
             traffic = None
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    if tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, world]:
+                    if (tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, world]
+                            and tj.get("accel") == ACCEL_TAG):
                         traffic = tj.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None

@@ -462,8 +462,7 @@ enum : int {
     CW_M = 13,                        // m0..m2 (f64, lo/hi words)
     CW_ACC = 19,                      // acc (f64 x 3)
     CW_WGT = 25,                      // wgt (f64 x 3)
-    CW_TRACED = 31, CW_REFERENCE, CW_SAMPLES, CW_FALLBACKS,
-    kColdWords = 35
+    kColdWords = 31
 };
 enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4 };
 
@@ -495,10 +494,21 @@ struct ColdRec {
 // kMinWaves: waves per SIMD the register allocation must allow (launch bound); 4 = 128 VGPRs,
 // 5 = 96, 6 = 80 -- more resident waves hide more memory latency, at the price of spilling
 // shading-phase values (the walk loop itself stays spill-free down to 96).
+// One event per active lane added to an LDS counter with a single atomic per wave.
+__device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
+{
+    const uint64_t m = __ballot(1);
+    if (lane == __ffsll((long long)m) - 1) atomicAdd(c, (unsigned long long)__popcll(m));
+}
+
 template <bool kCount, int kMinWaves>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
     extern __shared__ uint32_t lds_wf[];
+    // block counters after the four stacks: traced, reference, samples, slow walks
+    unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * a.stack_words);
+    if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int D = a.bounces;
     Counters cnt;
@@ -520,7 +530,6 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.spill_stride * 4u), 0x00020000),
                     (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.spill_stride * 4u};
-    for (int k = 0; k < kColdWords; ++k) R.st(k, 0u);
 
     for (;;) {
         // ---------------------------------------------------------------- walk
@@ -545,27 +554,22 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         }
 
         // ---------------------------------------------------------------- shade + refill
+        // Only the per-bounce part of the shading state is held in registers here (sample
+        // index, bounce, flags, RNG, path weight); accumulator, running mean, pixel and memo
+        // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
-        const bool cold = state != ST_TRACE && state != ST_DONE;
-        if (cold) {
-            uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
+        if (state != ST_TRACE && state != ST_DONE) {
             int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
             uint32_t fl = R.ld(CW_FLAGS);
-            int32_t mtri = (int32_t)R.ld(CW_MTRI);
-            float mt = __uint_as_float(R.ld(CW_MT));
             Rng rng;
             rng.d = R.ld(CW_RNG); rng.v0 = R.ld(CW_RNG + 1); rng.v1 = R.ld(CW_RNG + 2);
             rng.v2 = R.ld(CW_RNG + 3); rng.v3 = R.ld(CW_RNG + 4); rng.v4 = R.ld(CW_RNG + 5);
-            double m0 = R.ldd(CW_M), m1 = R.ldd(CW_M + 2), m2 = R.ldd(CW_M + 4);
-            C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
             C3 wgt = c3(R.ldd(CW_WGT), R.ldd(CW_WGT + 2), R.ldd(CW_WGT + 4));
-            uint32_t traced = R.ld(CW_TRACED), reference = R.ld(CW_REFERENCE);
-            uint32_t samples = R.ld(CW_SAMPLES), fallbacks = R.ld(CW_FALLBACKS);
 
             // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
             // a ray outside the Markstein preconditions, which takes the exact slow walk)
             auto begin_trace = [&](V3 o, V3 d) -> bool {
-                ++traced;
+                wave_count(lcnt + 0, lane);
                 if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
                 if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
                     htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
@@ -573,18 +577,19 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 state = ST_TRACE;
                 return false;
             };
-            // start sample n of the current pixel: camera ray, then memo or trace
-            auto start_sample = [&]() -> bool {
+            // start sample n of pixel (px, py): camera ray, then memo or trace
+            auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
                 i = 0;
-                acc = c3(0, 0, 0);
+                R.std_(CW_ACC, 0.0); R.std_(CW_ACC + 2, 0.0); R.std_(CW_ACC + 4, 0.0);
                 wgt = c3(1, 1, 1);
                 float u1 = 0.0f, u2 = 0.0f;
                 const bool lens = (fl & CF_LENS) != 0u;
                 if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
                 camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
-                ++reference;
+                wave_count(lcnt + 1, lane);
                 if (fl & CF_HAVE) {
-                    htri = mtri; ht = mt; fl &= ~CF_PRIMARY; state = ST_SHADE;
+                    htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
+                    fl &= ~CF_PRIMARY; state = ST_SHADE;
                     return true;
                 }
                 fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
@@ -595,14 +600,14 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             while (again) {
                 again = false;
                 if (state == ST_SLOW) {
-                    ++fallbacks;
+                    wave_count(lcnt + 3, lane);
                     trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
                                &htri, &ht);
                 }
                 state = ST_SHADE;
                 if (fl & CF_PRIMARY) {
                     fl = (fl | CF_HAVE) & ~CF_PRIMARY;
-                    mtri = htri; mt = ht;
+                    R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
                 }
                 // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
                 {
@@ -615,7 +620,9 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     const V3 normal = ld_norm(a.shade, tri);
                     const V3 pos = ro + rd * t;
                     if (cm->emission[0] != 0) {
+                        C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
                         acc = cadd(acc, cmul(wgt, mat_emission(cm)));
+                        R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
                         wgt = c3(0, 0, 0);
                     }
                     V3 ldir;
@@ -642,11 +649,12 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 for (;;) {
                     if (i >= D) {
                         const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
-                        m0 = (m0 * fn1) / fn + acc.r / fn;
-                        m1 = (m1 * fn1) / fn + acc.g / fn;
-                        m2 = (m2 * fn1) / fn + acc.b / fn;
-                        ++samples;
+                        const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
+                        const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
+                        const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
+                        wave_count(lcnt + 2, lane);
                         if (n >= a.spp) {
+                            const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
                             float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
                             o3[0] = (float)m0;
                             o3[1] = (float)m1;
@@ -654,19 +662,20 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                             state = ST_IDLE;
                             break;
                         }
+                        R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
                         ++n;
-                        again = start_sample();
+                        again = start_sample(R.ld(CW_PX), R.ld(CW_PY));
                         break;
                     }
                     if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
-                        ++reference;
+                        wave_count(lcnt + 1, lane);
                         const float u = rng_uniform(rng);
                         if (u < 0.5) { rng_next(rng); rng_next(rng); }
                         else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
                         ++i;
                         continue;
                     }
-                    ++reference;
+                    wave_count(lcnt + 1, lane);
                     again = begin_trace(ro, rd);
                     break;
                 }
@@ -689,48 +698,42 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                         const uint32_t l = u & 63u;
                         const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
                         const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
-                        px = (t % a.tiles_x) * kTile + qx;
-                        py = (t / a.tiles_x) * kTile + qy;
+                        const uint32_t px = (t % a.tiles_x) * kTile + qx;
+                        const uint32_t py = (t / a.tiles_x) * kTile + qy;
                         if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
                             const uint32_t idx = morton2(px, py);
                             rng_init(rng, a.seed, idx, a.jump);
                             fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
                             n = 1;
-                            m0 = m1 = m2 = 0.0;
-                            start_sample();
+                            R.st(CW_PX, px); R.st(CW_PY, py);
+                            R.std_(CW_M, 0.0); R.std_(CW_M + 2, 0.0); R.std_(CW_M + 4, 0.0);
+                            start_sample(px, py);
                         }
                     }
                 }
             }
 
-            R.st(CW_PX, px); R.st(CW_PY, py); R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i);
-            R.st(CW_FLAGS, fl); R.st(CW_MTRI, (uint32_t)mtri); R.st(CW_MT, __float_as_uint(mt));
+            R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i); R.st(CW_FLAGS, fl);
             R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
             R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
-            R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
-            R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
             R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
-            R.st(CW_TRACED, traced); R.st(CW_REFERENCE, reference);
-            R.st(CW_SAMPLES, samples); R.st(CW_FALLBACKS, fallbacks);
         }
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
-    const unsigned long long c0 = wave_sum(R.ld(CW_TRACED)), c1 = wave_sum(R.ld(CW_REFERENCE));
-    const unsigned long long c4 = wave_sum(R.ld(CW_SAMPLES)), c8 = wave_sum(R.ld(CW_FALLBACKS));
-    unsigned long long c2 = 0, c3v = 0, c5 = 0, c6 = 0, c7 = 0;
     if (kCount) {
-        c2 = wave_sum(cnt.nodes); c3v = wave_sum(cnt.tris); c5 = wave_sum(walk_slots);
-        c6 = wave_sum(cnt.leaf_steps); c7 = wave_sum(shade_slots);
-    }
-    if (lane == 0) {
-        atomicAdd(a.counters + 0, c0);
-        atomicAdd(a.counters + 1, c1);
-        atomicAdd(a.counters + 4, c4);
-        if (c8) atomicAdd(a.counters + 8, c8);
-        if (kCount) {
+        const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
+        const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
+        if (lane == 0) {
             atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
             atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
         }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(a.counters + 0, lcnt[0]);
+        atomicAdd(a.counters + 1, lcnt[1]);
+        atomicAdd(a.counters + 4, lcnt[2]);
+        if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
     }
 }
 
@@ -861,9 +864,9 @@ struct pt_ctx {
     uint32_t* pixel_counter = nullptr;
     bool scene_fast = false;
     uint32_t node_mask = 0;
-    uint32_t wf_threshold = 24;
+    uint32_t wf_threshold = 60;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
     uint32_t wf_waves_per_cu = 16;
-    int wf_min_waves = 4;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
+    int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
@@ -1019,7 +1022,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
             const int v = atoi(e);
-            c->wf_min_waves = (v == 5 || v == 6) ? v : 4;
+            c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
         }
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
@@ -1192,7 +1195,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         Args b = a;
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
-        const size_t lds_wf = (size_t)b.stack_words * 4 * 4;
+        const size_t lds_wf = (size_t)b.stack_words * 4 * 4 + 4 * sizeof(unsigned long long);
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         const uint32_t need = (a.nunits + 255) / 256;
         if (blocks > need) blocks = need;
@@ -1201,7 +1204,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.spill = c->spill;
         b.spill_stride = blocks * 256;
         b.cold = c->spill + per_lane * (size_t)b.spill_stride;
-        if (count) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
