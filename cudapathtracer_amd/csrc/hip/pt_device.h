@@ -570,16 +570,17 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const uint4 ch = nd->child;
     if (kCount) ++cnt.nodes;
     float lim = w.best_t * cull_rel;
-    float t0 = (ch.x == kEmpty) ? INFINITY : box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
-    float t1 = (ch.y == kEmpty) ? INFINITY : box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
-    float t2 = (ch.z == kEmpty) ? INFINITY : box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
-    float t3 = (ch.w == kEmpty) ? INFINITY : box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
+    // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
+    float t0 = box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
+    float t1 = box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
+    float t2 = box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
+    float t3 = box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
     uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
     // leaf children whose (inflated) box is entered: exact triangle test, one at a time
-    uint32_t leaves = ((r0 & kLeaf) && r0 != kEmpty && t0 != INFINITY ? 1u : 0u) |
-                      ((r1 & kLeaf) && r1 != kEmpty && t1 != INFINITY ? 2u : 0u) |
-                      ((r2 & kLeaf) && r2 != kEmpty && t2 != INFINITY ? 4u : 0u) |
-                      ((r3 & kLeaf) && r3 != kEmpty && t3 != INFINITY ? 8u : 0u);
+    uint32_t leaves = ((r0 & kLeaf) && t0 != INFINITY ? 1u : 0u) |
+                      ((r1 & kLeaf) && t1 != INFINITY ? 2u : 0u) |
+                      ((r2 & kLeaf) && t2 != INFINITY ? 4u : 0u) |
+                      ((r3 & kLeaf) && t3 != INFINITY ? 8u : 0u);
     while (leaves) {
         const uint32_t c = __builtin_ctz(leaves);
         leaves &= leaves - 1u;

@@ -226,8 +226,11 @@ struct Collapser {
         Accel4Node& nd = out.nodes[me];
         for (int k = 0; k < 4; ++k) {
             for (int ax = 0; ax < 3; ++ax) {
-                nd.lo[ax][k] = (k < n) ? c[k].box[ax] : INFINITY;
-                nd.hi[ax][k] = (k < n) ? c[k].box[3 + ax] : -INFINITY;
+                // empty slot: a point at 2^100 -- every ray rejects it (entry >= 2^99 beyond any
+                // best distance, or exit behind the origin; o*inv stays finite, so no NaN), which
+                // keeps the kernel's four box tests branch-free
+                nd.lo[ax][k] = (k < n) ? c[k].box[ax] : 0x1p100f;
+                nd.hi[ax][k] = (k < n) ? c[k].box[3 + ax] : 0x1p100f;
             }
             nd.child[k] = refs[k];
         }
