@@ -201,7 +201,9 @@ def main():
                     "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"]),
                     "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
                     "leaf_step_frac": round(counts["leaf_steps"] / max(counts["node_tests"], 1), 4),
-                    "accel_fallbacks": int(counts["accel_fallbacks"])}
+                    "accel_fallbacks": int(counts["accel_fallbacks"]),
+                    "walk_phase_frac": round(counts["walk_cycles"] / max(counts["walk_cycles"] + counts["shade_cycles"], 1), 4),
+                    "shade_phases": int(counts["shade_lane_slots"] // 64)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget)

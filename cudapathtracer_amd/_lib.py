@@ -20,6 +20,7 @@ PT_FLAG_NO_DEAD_PATH_SKIP = 0x2
 PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
+ABI_VERSION = 2                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -61,7 +62,8 @@ class Stats(C.Structure):
     _fields_ = [("seconds", C.c_double), ("kernel_ms", C.c_double), ("samples", C.c_uint64),
                 ("rays_traced", C.c_uint64), ("rays_reference", C.c_uint64), ("rays_nominal", C.c_uint64),
                 ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("walk_lane_slots", C.c_uint64),
-                ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64)]
+                ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64),
+                ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -111,6 +113,8 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        if handle.pt_abi_version() != ABI_VERSION:
+            raise RuntimeError("libptamd.so ABI %d, bindings expect %d: rebuild it" % (handle.pt_abi_version(), ABI_VERSION))
         _lib = handle
     return _lib
 

@@ -163,31 +163,38 @@ __device__ __forceinline__ float rng_uniform(Rng& s)
 
 // curand_init(seed, subsequence, 0) (kernel.cu:532): cuRAND seeding salts, then
 // v <- A^(subsequence * 2^67) v through the tables J_k = A^(2^(67+k)) (160 rows x 5 words).
-__device__ __forceinline__ void rng_init(Rng& s, uint64_t seed, uint32_t subseq, const uint32_t* __restrict__ jump)
+// curand_init(seed, subseq, 0) (kernel.cu:532): seed scrambling, then v <- J_k v for every set
+// bit k of subseq, J_k = A^(2^(67+k)).  J_k is applied byte-sliced: jb holds, for each k and
+// each of the 20 state bytes j, the 256 products J_k * (x << 8j) (5 words padded to 8), so a
+// jump is 20 independent 32-B lookups XORed together -- no data-dependent bit loop.
+constexpr int kJumpEntryWords = 8;
+__device__ __forceinline__ uint32_t rng_seed_d(uint64_t seed)
 {
-    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
-    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
-    const uint32_t t0 = 1099087573u * s0;
-    const uint32_t t1 = 2591861531u * s1;
+    const uint32_t t0 = 1099087573u * ((uint32_t)seed ^ 0xaad26b49u);
+    const uint32_t t1 = 2591861531u * ((uint32_t)(seed >> 32) ^ 0xf7dcefddu);
+    return 6615241u + t1 + t0;
+}
+__device__ __forceinline__ void rng_init(Rng& s, uint64_t seed, uint32_t subseq, const uint32_t* __restrict__ jb)
+{
+    const uint32_t t0 = 1099087573u * ((uint32_t)seed ^ 0xaad26b49u);
+    const uint32_t t1 = 2591861531u * ((uint32_t)(seed >> 32) ^ 0xf7dcefddu);
     s.d = 6615241u + t1 + t0;
-    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    uint32_t v0 = 123456789u + t0, v1 = 362436069u ^ t0, v2 = 521288629u + t1, v3 = 88675123u ^ t1, v4 = 5783321u + t0;
     for (int k = 0; k < 32; ++k) {
         if (!((subseq >> k) & 1u)) continue;
-        const uint32_t* m = jump + (size_t)k * 800;
+        const uint32_t* m = jb + (size_t)k * (20 * 256 * kJumpEntryWords);
         uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
 #pragma unroll
-        for (int w = 0; w < 5; ++w) {
-            uint32_t bits = v[w];
-            while (bits) {
-                const int b = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t* row = m + (w * 32 + b) * 5;
-                r0 ^= row[0]; r1 ^= row[1]; r2 ^= row[2]; r3 ^= row[3]; r4 ^= row[4];
-            }
+        for (int j = 0; j < 20; ++j) {
+            const uint32_t w = (j < 4) ? v0 : (j < 8) ? v1 : (j < 12) ? v2 : (j < 16) ? v3 : v4;
+            const uint32_t x = (w >> (8 * (j & 3))) & 255u;
+            const uint32_t* e = m + ((size_t)j * 256 + x) * kJumpEntryWords;
+            const uint4 q = *reinterpret_cast<const uint4*>(e);
+            r0 ^= q.x; r1 ^= q.y; r2 ^= q.z; r3 ^= q.w; r4 ^= e[4];
         }
-        v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+        v0 = r0; v1 = r1; v2 = r2; v3 = r3; v4 = r4;
     }
-    s.v0 = v[0]; s.v1 = v[1]; s.v2 = v[2]; s.v3 = v[3]; s.v4 = v[4];
+    s.v0 = v0; s.v1 = v1; s.v2 = v2; s.v3 = v3; s.v4 = v4;
 }
 
 // ------------------------------------------------------------------ geometry tests

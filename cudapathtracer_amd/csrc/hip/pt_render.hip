@@ -60,6 +60,7 @@ struct Args {
     uint32_t spill_stride;
     float acc_root[6];
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
+    const uint32_t* pix_states;     // XORWOW v0..v4 of each work unit, word k of unit u at [k*nunits + u]
 };
 
 // ------------------------------------------------------------------ per-lane tracer
@@ -494,6 +495,29 @@ struct ColdRec {
 // kMinWaves: waves per SIMD the register allocation must allow (launch bound); 4 = 128 VGPRs,
 // 5 = 96, 6 = 80 -- more resident waves hide more memory latency, at the price of spilling
 // shading-phase values (the walk loop itself stays spill-free down to 96).
+// setupCurand (kernel.cu:527-533) for the wavefront kernel: the XORWOW state of every work unit
+// (pixel) of this shard, computed in parallel before the render so that a lane starting a pixel
+// inside the state machine loads 20 B instead of running the jump-ahead with its wave waiting.
+__global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __restrict__ st)
+{
+    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
+    if (u >= a.nunits) return;
+    const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
+    const uint32_t l = u & 63u;
+    const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
+    const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
+    const uint32_t px = (t % a.tiles_x) * kTile + qx;
+    const uint32_t py = (t / a.tiles_x) * kTile + qy;
+    if (px >= (uint32_t)a.w || py >= (uint32_t)a.h) return;
+    Rng r;
+    rng_init(r, a.seed, morton2(px, py), a.jump);
+    st[u] = r.v0;
+    st[(size_t)a.nunits + u] = r.v1;
+    st[2 * (size_t)a.nunits + u] = r.v2;
+    st[3 * (size_t)a.nunits + u] = r.v3;
+    st[4 * (size_t)a.nunits + u] = r.v4;
+}
+
 // One event per active lane added to an LDS counter with a single atomic per wave.
 __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 {
@@ -516,6 +540,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     cnt.tris = 0;
     cnt.leaf_steps = 0;
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
+    unsigned long long walk_clk = 0, shade_clk = 0;   // counting variant: wave-clock per phase
 
     // hot state: what the walk phase needs
     uint32_t state = ST_IDLE;
@@ -533,6 +558,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 
     for (;;) {
         // ---------------------------------------------------------------- walk
+        unsigned long long clk0 = 0;
+        if (kCount) clk0 = clock64();
         for (;;) {
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
@@ -553,6 +580,11 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             }
         }
 
+        if (kCount) {
+            const unsigned long long c = clock64();
+            walk_clk += c - clk0;
+            clk0 = c;
+        }
         // ---------------------------------------------------------------- shade + refill
         // Only the per-bounce part of the shading state is held in registers here (sample
         // index, bounce, flags, RNG, path weight); accumulator, running mean, pixel and memo
@@ -702,7 +734,13 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                         const uint32_t py = (t / a.tiles_x) * kTile + qy;
                         if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
                             const uint32_t idx = morton2(px, py);
-                            rng_init(rng, a.seed, idx, a.jump);
+                            // curand_init's state, computed for every unit by init_pixel_states
+                            rng.d = rng_seed_d(a.seed);
+                            rng.v0 = a.pix_states[u];
+                            rng.v1 = a.pix_states[(size_t)a.nunits + u];
+                            rng.v2 = a.pix_states[2 * (size_t)a.nunits + u];
+                            rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
+                            rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
                             fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
                             n = 1;
                             R.st(CW_PX, px); R.st(CW_PY, py);
@@ -718,9 +756,11 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
             R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
         }
+        if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
     if (kCount) {
+        if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
         if (lane == 0) {
@@ -837,6 +877,20 @@ static void build_jump_tables(std::vector<uint32_t>& out)
     }
 }
 
+// Byte-sliced form of the jump tables for rng_init: entry (k, j, x) = J_k * (x << 8j).
+static void build_jump_bytes(const std::vector<uint32_t>& img, std::vector<uint32_t>& out)
+{
+    out.assign((size_t)32 * 20 * 256 * kJumpEntryWords, 0u);
+    for (int k = 0; k < 32; ++k)
+        for (int j = 0; j < 20; ++j)
+            for (int x = 0; x < 256; ++x) {
+                uint32_t* e = &out[(((size_t)k * 20 + j) * 256 + x) * kJumpEntryWords];
+                for (int i = 0; i < 8; ++i)
+                    if ((x >> i) & 1)
+                        for (int w = 0; w < 5; ++w) e[w] ^= img[(size_t)k * 800 + (8 * j + i) * 5 + w];
+            }
+}
+
 void pt::sincos_det(float theta, float* s, float* c) { det_sincos(theta, s, c); }
 
 struct pt_ctx {
@@ -872,6 +926,8 @@ struct pt_ctx {
     uint32_t* rparent = nullptr;
     uint32_t* spill = nullptr;
     size_t spill_words = 0;
+    uint32_t* pix_states = nullptr;   // init_pixel_states output (5 words per work unit)
+    size_t pix_states_words = 0;
     float acc_root[6];
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
@@ -1091,8 +1147,9 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     lt[sc->num_lights] = light_rec(0);
     c->num_lights = sc->num_lights;
     c->total_light_area = sc->total_light_area;
-    std::vector<uint32_t> jump;
-    build_jump_tables(jump);
+    std::vector<uint32_t> jump_img, jump;
+    build_jump_tables(jump_img);
+    build_jump_bytes(jump_img, jump);
 
     int rc = PT_OK;
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
@@ -1119,7 +1176,7 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->nodes4, c->acc_tris, c->rparent, c->spill};
+                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1204,6 +1261,16 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.spill = c->spill;
         b.spill_stride = blocks * 256;
         b.cold = c->spill + per_lane * (size_t)b.spill_stride;
+        const size_t sw = (size_t)5 * a.nunits;
+        if (c->pix_states_words < sw) {
+            if (c->pix_states) (void)hipFree(c->pix_states);
+            c->pix_states = nullptr;
+            c->pix_states_words = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pix_states), sw * 4));
+            c->pix_states_words = sw;
+        }
+        b.pix_states = c->pix_states;
+        hipLaunchKernelGGL(init_pixel_states, dim3((a.nunits + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
         if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
@@ -1240,6 +1307,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         st->leaf_steps = cnt[6];
         st->shade_lane_slots = cnt[7];
         st->accel_fallbacks = cnt[8];
+        st->walk_cycles = cnt[9];
+        st->shade_cycles = cnt[10];
         const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
         st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
     }

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 /* ---- status codes */
 #define PT_OK 0
@@ -154,8 +154,12 @@ typedef struct {
                                   node_tests gives the SIMD lane utilisation of the walk          */
     uint64_t leaf_steps;       /* PT_FLAG_COUNT: walk steps that tested a triangle                */
     uint64_t shade_lane_slots; /* PT_FLAG_COUNT, wavefront kernel: 64 x shading passes            */
-    uint64_t accel_fallbacks;  /* rays re-walked on the reference BVH after the SAH walk's winner
-                                  failed the reference-parent check                              */
+    uint64_t accel_fallbacks;  /* rays taking the exact reference-BVH walk: outside the fast-path
+                                  preconditions, or the BVH4 winner failed the reference-parent
+                                  check                                                          */
+    uint64_t walk_cycles;      /* PT_FLAG_COUNT, wavefront kernel: wave-clock cycles spent in walk
+                                  phases, summed over waves                                     */
+    uint64_t shade_cycles;     /* same for shading (+ refill) phases                              */
 } pt_stats;
 
 /* Upload a scene to HIP device `device` (ordinal among visible devices). */
