@@ -309,6 +309,40 @@ __device__ __forceinline__ bool slab(V3 o, V3 d, V3 y, float lx, float ly, float
     return true;
 }
 
+// Materialise a loaded value here: keeps the compiler from sinking the load into the branch
+// that first uses it (which would turn one memory round trip into several dependent ones).
+__device__ __forceinline__ void pin(float4& v)
+{
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
+// triIntersect (modelLoader.h:49-83) on a record already in registers; kMk: one IEEE
+// reciprocal of `a`, Markstein quotients.
+template <bool kMk>
+__device__ __forceinline__ float tri_hit_rec(V3 o, V3 d, float4 A, float4 B, float4 C)
+{
+    const V3 v0 = v3(A.x, A.y, A.z), e1 = v3(A.w, B.x, B.y), e2 = v3(B.z, B.w, C.x);
+    const V3 q = cross(d, e2);
+    const float a = dot(e1, q);
+    if ((double)__builtin_fabsf(a) < 0.00001) return kMaxFloat;
+    const V3 w = o - v0;
+    V3 s;
+    if (kMk) {
+        const float ya = 1.0f / a;
+        s = v3(div_mk(w.x, a, ya), div_mk(w.y, a, ya), div_mk(w.z, a, ya));
+    } else {
+        s = w / a;
+    }
+    const V3 r = cross(s, e1);
+    const float b0 = dot(s, q);
+    const float b1 = dot(r, d);
+    const float b2 = 1.0f - b0 - b1;
+    if (b0 < 0.0f) return kMaxFloat;
+    if (b1 < 0.0f) return kMaxFloat;
+    if (b2 < 0.0f) return kMaxFloat;
+    return dot(e2, r);
+}
+
 // triIntersect (modelLoader.h:49-83); kMk: one IEEE reciprocal of `a`, Markstein quotients.
 template <bool kMk>
 __device__ __forceinline__ float tri_hit(V3 o, V3 d, const DTri* __restrict__ tr, uint32_t* id)
@@ -551,7 +585,7 @@ struct Stack4 {
 
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 {
-    const int slot = (w.sp % kRing) * 64 + S.lane;
+    const int slot = (w.sp & (kRing - 1)) * 64 + S.lane;   // sp >= 0, kRing a power of two
     if (w.sp >= kRing) S.spill[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
     S.ring[slot] = e;
     ++w.sp;
@@ -560,7 +594,7 @@ __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 {
     --w.sp;
-    const int slot = (w.sp % kRing) * 64 + S.lane;
+    const int slot = (w.sp & (kRing - 1)) * 64 + S.lane;
     const uint32_t e = S.ring[slot];
     if (w.sp >= kRing) S.ring[slot] = S.spill[(size_t)(w.sp - kRing) * S.stride];
     return e;
@@ -593,12 +627,13 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         leaves &= leaves - 1u;
         const uint32_t r = (c == 0u) ? r0 : (c == 1u) ? r1 : (c == 2u) ? r2 : r3;
         const DTri* tr = tris + (r ^ kLeaf);
-        uint32_t id;
-        const float t = tri_hit<true>(o, d, tr, &id);
+        float4 A = tr->a, B = tr->b, C = tr->c;   // one round trip for the whole record
+        pin(A); pin(B); pin(C);
+        const float t = tri_hit_rec<true>(o, d, A, B, C);
         if (kCount) { ++cnt.tris; if (leaves == 0u) ++cnt.leaf_steps; }
-        const uint32_t rank = __float_as_uint(tr->c.z);
+        const uint32_t rank = __float_as_uint(C.z);
         if (0.0f < t && (t < w.best_t || (t == w.best_t && rank < w.best_rank))) {
-            w.best_t = t; w.best_rank = rank; w.best_id = id; w.best_parent = __float_as_uint(tr->c.w);
+            w.best_t = t; w.best_rank = rank; w.best_id = __float_as_uint(C.y); w.best_parent = __float_as_uint(C.w);
         }
     }
     // inner children, nearest first; entries beyond the (possibly improved) best are dropped
