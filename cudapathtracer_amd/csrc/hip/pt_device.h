@@ -315,6 +315,10 @@ __device__ __forceinline__ void pin(float4& v)
 {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
+__device__ __forceinline__ void pin(uint4& v)
+{
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
 
 // triIntersect (modelLoader.h:49-83) on a record already in registers; kMk: one IEEE
 // reciprocal of `a`, Markstein quotients.
@@ -371,123 +375,6 @@ __device__ __forceinline__ float tri_hit(V3 o, V3 d, const DTri* __restrict__ tr
     return dot(e2, r);
 }
 
-// Resumable state of the culled near-first walk (trace_culled below, one node per step).
-struct Walk {
-    V3 y;                 // y = RN(1/d) of the ray being walked (the ray itself stays with the caller)
-    uint32_t node;        // current node record
-    int32_t sp;           // LDS stack depth
-    uint32_t tree;        // 0 = render-path SAH BVH, 1 = the reference BVH (exact fallback)
-    float best_t;
-    uint32_t best_rank, best_id, best_parent;
-};
-
-// The two node/triangle arrays a walk can run on.
-struct Trees {
-    const DNode* nodes[2];
-    const DTri* tris[2];
-    const float* root[2];
-};
-
-// Start a walk: root box test (the reference tests node 0's own box first).  Returns false
-// when the ray misses the root (walk finished, no hit).
-// best_rank starts at 0 so a tie with the MAX_FLOAT sentinel is never accepted (the reference
-// needs t < closestT = MAX_FLOAT); best_id = ~0 marks "no hit yet".
-template <bool kMk>
-__device__ __forceinline__ bool walk_begin(Walk& w, V3 o, V3 d, const float* root, float cull_abs)
-{
-    w.y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    w.node = 0; w.sp = 0;
-    w.best_t = kMaxFloat; w.best_rank = 0u; w.best_id = 0xffffffffu; w.best_parent = 0u;
-    float ti, to;
-    return slab<kMk>(o, d, w.y, root[0], root[1], root[2], root[3], root[4], root[5], &ti, &to) && !(to < -cull_abs);
-}
-
-// Candidate update shared by the walks: minimum of (t, reference DFS rank) over 0 < t.
-__device__ __forceinline__ void take_hit(Walk& w, float t, const DTri* __restrict__ tr, uint32_t id)
-{
-    const uint32_t rank = __float_as_uint(tr->c.z);
-    if (0.0f < t && (t < w.best_t || (t == w.best_t && rank < w.best_rank))) {
-        w.best_t = t; w.best_rank = rank; w.best_id = id; w.best_parent = __float_as_uint(tr->c.w);
-    }
-}
-
-// One node of the walk.  Returns true while the walk continues.
-template <bool kMk, bool kCount>
-__device__ __forceinline__ bool walk_step(Walk& w, V3 o, V3 d, const Trees& T, uint32_t* stack, int lane,
-                                          float cull_rel, float cull_abs, uint32_t node_mask, Counters& cnt)
-{
-    const DNode* nodes = w.tree ? T.nodes[1] : T.nodes[0];
-    const DTri* tris = w.tree ? T.tris[1] : T.tris[0];
-    const DNode* nd = nodes + w.node;
-    const float4 A = nd->a, B = nd->b, C = nd->c;
-    const uint4 D = nd->d;
-    if (kCount) { ++cnt.nodes; if ((D.x | D.y) & kLeaf) ++cnt.leaf_steps; }
-    float ti, to, t0 = 0.0f, t1 = 0.0f;
-    bool h0 = false, h1 = false;
-    if (D.x & kLeaf) {
-        const DTri* tr = tris + (D.x ^ kLeaf);
-        uint32_t id;
-        const float t = tri_hit<kMk>(o, d, tr, &id);
-        if (kCount) ++cnt.tris;
-        take_hit(w, t, tr, id);
-    } else {
-        h0 = slab<kMk>(o, d, w.y, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to) && !(to < -cull_abs) &&
-             !(ti > w.best_t * cull_rel);
-        t0 = ti;
-    }
-    if (D.y & kLeaf) {
-        const DTri* tr = tris + (D.y ^ kLeaf);
-        uint32_t id;
-        const float t = tri_hit<kMk>(o, d, tr, &id);
-        if (kCount) ++cnt.tris;
-        take_hit(w, t, tr, id);
-        h0 = h0 && !(t0 > w.best_t * cull_rel);
-    } else {
-        h1 = slab<kMk>(o, d, w.y, B.z, B.w, C.x, C.y, C.z, C.w, &ti, &to) && !(to < -cull_abs) &&
-             !(ti > w.best_t * cull_rel);
-        t1 = ti;
-    }
-    // LDS stack entry: far child's node index in the low node_bits, the top bits of its entry
-    // distance above them (its float truncated toward zero: a lower bound for t >= 0, so the
-    // pop-time cull stays conservative).  node_bits <= 23 keeps sign and exponent intact.
-    if (h0 && h1) {
-        const bool swap = t1 < t0;
-        const uint32_t far_node = swap ? D.x : D.y;
-        const uint32_t far_t = __float_as_uint(swap ? t0 : t1);
-        stack[w.sp * 64 + lane] = (far_t & ~node_mask) | far_node;
-        ++w.sp;
-        w.node = swap ? D.y : D.x;
-        return true;
-    }
-    if (h0 | h1) { w.node = h0 ? D.x : D.y; return true; }
-    while (w.sp > 0) {
-        --w.sp;
-        const uint32_t e = stack[w.sp * 64 + lane];
-        const float et = __uint_as_float(e & ~node_mask);
-        if (et > w.best_t * cull_rel) continue;
-        w.node = e & node_mask;
-        return true;
-    }
-    return false;
-}
-
-// Winner check for a walk on the render-path BVH: the reference tests a triangle iff the line
-// passes the slab test of every ancestor of its leaf in the reference BVH.  Slab values are
-// correctly rounded, hence monotone in the box bounds, and every ancestor box contains its
-// descendants, so (with no NaN: fast rays have no zero direction component) the parent's test
-// passing implies all ancestors pass.  Returns true when the current best is a triangle the
-// reference would have tested (or there is no hit).
-template <bool kMk>
-__device__ __forceinline__ bool winner_ok(const Walk& w, V3 o, V3 d, const RNode* __restrict__ rnodes)
-{
-    if (w.best_id == 0xffffffffu) return true;
-    const RNode* p = rnodes + w.best_parent;
-    const float4 a = *reinterpret_cast<const float4*>(p);
-    const float4 b = *reinterpret_cast<const float4*>(&p->hi[1]);
-    float ti, to;
-    return slab<kMk>(o, d, w.y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to);
-}
-
 // ------------------------------------------------------------------ 4-wide render-path walk
 // Node of the render-path BVH4 (collapsed SAH BVH): 4 child boxes SoA + 4 child refs, 128 B.
 struct alignas(16) DNode4 {
@@ -497,26 +384,28 @@ struct alignas(16) DNode4 {
 };
 static_assert(sizeof(DNode4) == 128, "BVH4 node is 128 B");
 constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr uint32_t kNone = 0xffffffffu;    // no node / no leaf pending
+constexpr int kLeafRing = 8;               // LDS leaf-queue entries per lane
 constexpr int kRing = 16;                 // LDS stack entries per lane; deeper entries spill to HBM
-
-enum : uint32_t { W4_FILTER = 1u, W4_ZERO_DIR = 2u, W4_FAST = 4u };
 
 struct W4 {
     V3 inv;              // RN(1/d): also the Markstein reciprocal for the exact checks
     V3 oi;               // o * inv, for the conservative box test t = fma(b, inv, -oi)
-    uint32_t node;
-    int32_t sp;
-    uint32_t flags;
+    uint32_t node;       // next node to visit, kNone = pop one
+    uint32_t leaf;       // next leaf (triangle slot) to test, kNone = none pending
+    int32_t sp;          // node stack depth
+    int32_t lsp;         // leaves queued in the LDS leaf ring (besides `leaf`)
     float best_t;
-    uint32_t best_rank, best_id, best_parent;
+    uint32_t best_slot;  // render-path triangle slot of the best hit, kNone = none
 };
 
 // The exact reference test a winner must pass (DESIGN.md "Traversal" 2): the reference slab test
 // on its reference parent -- or, when a direction component is 0 (NaN slab values possible),
 // on every ancestor up the reference tree.
-__device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d, uint32_t flags,
+__device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
                                            const RNode* __restrict__ rnodes, const uint32_t* __restrict__ rparent)
 {
+    const bool zero_dir = d.x == 0.0f || d.y == 0.0f || d.z == 0.0f;
     const V3 y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // IEEE reciprocals: div_mk's y
     uint32_t n = parent;
     for (;;) {
@@ -525,7 +414,7 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d, uint32_t
         const float4 b = *reinterpret_cast<const float4*>(&p->hi[1]);
         float ti, to;
         if (!slab<true>(o, d, y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to)) return false;
-        if (!(flags & W4_ZERO_DIR) || n == 0u) return true;
+        if (!zero_dir || n == 0u) return true;
         n = rparent[n];
     }
 }
@@ -544,9 +433,8 @@ __device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root
     if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, w.inv.y);
     if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, w.inv.z);
     w.oi = v3(o.x * w.inv.x, o.y * w.inv.y, o.z * w.inv.z);
-    w.node = 0; w.sp = 0;
-    w.flags = W4_FAST | ((d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) ? W4_ZERO_DIR : 0u);
-    w.best_t = kMaxFloat; w.best_rank = 0u; w.best_id = 0xffffffffu; w.best_parent = 0u;
+    w.node = 0; w.leaf = kNone; w.sp = 0; w.lsp = 0;
+    w.best_t = kMaxFloat; w.best_slot = kNone;
     // conservative root test (boxes inflated; NaN planes are ignored by min/max)
     const float x0 = __builtin_fmaf(root[0], w.inv.x, -w.oi.x), x1 = __builtin_fmaf(root[3], w.inv.x, -w.oi.x);
     const float y0 = __builtin_fmaf(root[1], w.inv.y, -w.oi.y), y1 = __builtin_fmaf(root[4], w.inv.y, -w.oi.y);
@@ -576,16 +464,18 @@ __device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32
     const uint32_t r = s ? rb : ra; rb = s ? ra : rb; ra = r;
 }
 
+// Per wave, LDS holds a node ring of kRing x 64 words followed by a leaf ring of kLeafRing x 64;
+// `ring` points at this lane's word 0 (wave base + lane).
 struct Stack4 {
-    uint32_t* ring;       // LDS: entry k of this lane at ring[(k % kRing) * 64 + lane]
-    uint32_t* spill;      // HBM: entry k >= kRing at spill[(k - kRing) * stride]
+    uint32_t* ring;       // LDS: node entry k at ring[(k % kRing) * 64], queued leaf k at ring[(kRing + k) * 64]
+    uint32_t* spill;      // HBM: node entry k >= kRing at spill[(k - kRing) * stride]
     uint32_t stride;
-    int lane;
 };
+constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
 
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 {
-    const int slot = (w.sp & (kRing - 1)) * 64 + S.lane;   // sp >= 0, kRing a power of two
+    const int slot = (w.sp & (kRing - 1)) * 64;   // sp >= 0, kRing a power of two
     if (w.sp >= kRing) S.spill[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
     S.ring[slot] = e;
     ++w.sp;
@@ -594,66 +484,85 @@ __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 {
     --w.sp;
-    const int slot = (w.sp & (kRing - 1)) * 64 + S.lane;
+    const int slot = (w.sp & (kRing - 1)) * 64;
     const uint32_t e = S.ring[slot];
     if (w.sp >= kRing) S.ring[slot] = S.spill[(size_t)(w.sp - kRing) * S.stride];
     return e;
 }
 
-// One BVH4 node.  Returns true while the walk continues.
+// One walk step.  Returns true while the walk continues.
+// A step fetches the next node AND the next pending leaf triangle in one memory round trip, tests
+// the triangle, then the node's four child boxes; entered leaf children are queued (tested in
+// later steps, overlapped with later node fetches), inner children are visited near-first.
+// Deferring a leaf test only delays best_t improvements, i.e. culls less: the result is the
+// same exact minimum.  A node is visited only while the leaf queue has room for its children.
 template <bool kCount>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt)
 {
-    const DNode4* nd = nodes + w.node;
-    const float4 lx = nd->lox, ly = nd->loy, lz = nd->loz, hx = nd->hix, hy = nd->hiy, hz = nd->hiz;
-    const uint4 ch = nd->child;
-    if (kCount) ++cnt.nodes;
-    float lim = w.best_t * cull_rel;
-    // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
-    float t0 = box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
-    float t1 = box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
-    float t2 = box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
-    float t3 = box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
-    uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
-    // leaf children whose (inflated) box is entered: exact triangle test, one at a time
-    uint32_t leaves = ((r0 & kLeaf) && t0 != INFINITY ? 1u : 0u) |
-                      ((r1 & kLeaf) && t1 != INFINITY ? 2u : 0u) |
-                      ((r2 & kLeaf) && t2 != INFINITY ? 4u : 0u) |
-                      ((r3 & kLeaf) && t3 != INFINITY ? 8u : 0u);
-    while (leaves) {
-        const uint32_t c = __builtin_ctz(leaves);
-        leaves &= leaves - 1u;
-        const uint32_t r = (c == 0u) ? r0 : (c == 1u) ? r1 : (c == 2u) ? r2 : r3;
-        const DTri* tr = tris + (r ^ kLeaf);
-        float4 A = tr->a, B = tr->b, C = tr->c;   // one round trip for the whole record
-        pin(A); pin(B); pin(C);
+    const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 4);
+    const bool leaf = w.leaf != kNone;
+    const DTri* tr = tris + (leaf ? w.leaf : 0u);
+    float4 A = tr->a, B = tr->b, C = tr->c;
+    const DNode4* nd = nodes + (visit ? w.node : 0u);
+    float4 lx = nd->lox, ly = nd->loy, lz = nd->loz, hx = nd->hix, hy = nd->hiy, hz = nd->hiz;
+    uint4 ch = nd->child;
+    pin(A); pin(B); pin(C);
+    pin(lx); pin(ly); pin(lz); pin(hx); pin(hy); pin(hz); pin(ch);
+    if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
+    if (leaf) {
         const float t = tri_hit_rec<true>(o, d, A, B, C);
-        if (kCount) { ++cnt.tris; if (leaves == 0u) ++cnt.leaf_steps; }
-        const uint32_t rank = __float_as_uint(C.z);
-        if (0.0f < t && (t < w.best_t || (t == w.best_t && rank < w.best_rank))) {
-            w.best_t = t; w.best_rank = rank; w.best_id = __float_as_uint(C.y); w.best_parent = __float_as_uint(C.w);
+        // ties go to the lower reference DFS rank (the reference's first-visited); exact ties are
+        // rare, so the best's rank is re-read rather than kept in a register
+        if (0.0f < t && (t < w.best_t ||
+                         (t == w.best_t && w.best_slot != kNone &&
+                          __float_as_uint(C.z) < __float_as_uint(tris[w.best_slot].c.z)))) {
+            w.best_t = t; w.best_slot = w.leaf;
+        }
+        w.leaf = kNone;
+    }
+    if (visit) {
+        float lim = w.best_t * cull_rel;
+        // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
+        float t0 = box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
+        float t1 = box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
+        float t2 = box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
+        float t3 = box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
+        uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
+        auto queue = [&](uint32_t slot) {
+            if (w.leaf == kNone) { w.leaf = slot; return; }
+            S.ring[(kRing + w.lsp) * 64] = slot;
+            ++w.lsp;
+        };
+        if ((r0 & kLeaf) && t0 != INFINITY) queue(r0 ^ kLeaf);
+        if ((r1 & kLeaf) && t1 != INFINITY) queue(r1 ^ kLeaf);
+        if ((r2 & kLeaf) && t2 != INFINITY) queue(r2 ^ kLeaf);
+        if ((r3 & kLeaf) && t3 != INFINITY) queue(r3 ^ kLeaf);
+        // inner children, nearest first; entries beyond the best are dropped
+        if (r0 & kLeaf) t0 = INFINITY;
+        if (r1 & kLeaf) t1 = INFINITY;
+        if (r2 & kLeaf) t2 = INFINITY;
+        if (r3 & kLeaf) t3 = INFINITY;
+        cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
+        if (t3 != INFINITY) push4(w, S, (__float_as_uint(t3) & ~node_mask) | r3);
+        if (t2 != INFINITY) push4(w, S, (__float_as_uint(t2) & ~node_mask) | r2);
+        if (t1 != INFINITY) push4(w, S, (__float_as_uint(t1) & ~node_mask) | r1);
+        w.node = (t0 != INFINITY) ? r0 : kNone;
+    }
+    if (w.leaf == kNone && w.lsp > 0) {
+        --w.lsp;
+        w.leaf = S.ring[(kRing + w.lsp) * 64];
+    }
+    if (w.node == kNone) {
+        while (w.sp > 0) {
+            const uint32_t e = pop4(w, S);
+            if (__uint_as_float(e & ~node_mask) > w.best_t * cull_rel) continue;
+            w.node = e & node_mask;
+            break;
         }
     }
-    // inner children, nearest first; entries beyond the (possibly improved) best are dropped
-    lim = w.best_t * cull_rel;
-    if ((r0 & kLeaf) || t0 > lim) t0 = INFINITY;
-    if ((r1 & kLeaf) || t1 > lim) t1 = INFINITY;
-    if ((r2 & kLeaf) || t2 > lim) t2 = INFINITY;
-    if ((r3 & kLeaf) || t3 > lim) t3 = INFINITY;
-    cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
-    if (t3 != INFINITY) push4(w, S, (__float_as_uint(t3) & ~node_mask) | r3);
-    if (t2 != INFINITY) push4(w, S, (__float_as_uint(t2) & ~node_mask) | r2);
-    if (t1 != INFINITY) push4(w, S, (__float_as_uint(t1) & ~node_mask) | r1);
-    if (t0 != INFINITY) { w.node = r0; return true; }
-    while (w.sp > 0) {
-        const uint32_t e = pop4(w, S);
-        if (__uint_as_float(e & ~node_mask) > w.best_t * cull_rel) continue;
-        w.node = e & node_mask;
-        return true;
-    }
-    return false;
+    return w.node != kNone || w.leaf != kNone;
 }
 
 // Exact walk for the rare rays the fast path does not take (outside the Markstein

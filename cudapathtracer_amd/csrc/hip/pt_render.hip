@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
 // direction, finishes samples / pixels and fetches new pixels.  Lanes therefore do not idle
 // until the slowest ray of the wave is done, which is where the tile kernel loses most time.
 // Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
-enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4 };
+enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4, ST_CHECK = 5 };
 
 // Per-lane shading state ("cold": not needed while the lane walks) lives in HBM, word k of lane g
 // at cold[k * stride + g] (coalesced), and is loaded/stored only around the shading phase, so the
@@ -529,8 +529,9 @@ template <bool kCount, int kMinWaves>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
     extern __shared__ uint32_t lds_wf[];
-    // block counters after the four stacks: traced, reference, samples, slow walks
-    unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * a.stack_words);
+    // after the four waves' rings (kWaveLdsWords each): the block counters (traced, reference,
+    // samples, slow walks)
+    unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords);
     if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -549,8 +550,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     int32_t htri = -1;
     float ht = kMaxFloat;
     Stack4 S;
-    S.ring = lds_wf + (threadIdx.x >> 6) * a.stack_words;
-    S.lane = lane;
+    S.ring = lds_wf + (threadIdx.x >> 6) * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
     S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.spill_stride * 4u), 0x00020000),
@@ -569,13 +569,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
                                                      a.node_mask, cnt);
                 if (!more) {
-                    htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
+                    // the winner's check against the reference BVH runs in the shading phase
+                    htri = (int32_t)w.best_slot;
                     ht = w.best_t;
-                    state = ST_SHADE;
-                    // the winner must be a triangle the reference tests; if not (rare), the exact
-                    // reference-BVH walk redoes the ray in the shading phase
-                    if (htri >= 0 && !ref_tested(w.best_parent, ro, rd, w.flags, a.rnodes, a.rparent))
-                        state = ST_SLOW;
+                    state = (w.best_slot == kNone) ? ST_SHADE : ST_CHECK;
                 }
             }
         }
@@ -591,6 +588,13 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
         if (state != ST_TRACE && state != ST_DONE) {
+            if (state == ST_CHECK) {
+                // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
+                // (rare), the exact reference-BVH walk redoes the ray
+                const float4 C = a.acc_tris[htri].c;
+                htri = (int32_t)__float_as_uint(C.y);
+                state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
+            }
             int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
             uint32_t fl = R.ld(CW_FLAGS);
             Rng rng;
@@ -790,8 +794,9 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
     Counters cnt;
     cnt.nodes = cnt.tris = cnt.leaf_steps = 0;
     Stack4 S;
-    S.ring = lds_tr + (threadIdx.x >> 6) * a.stack_words;
-    S.lane = lane;
+    // per wave: the reference walk's stack (stack_words) or the BVH4 rings (kWaveLdsWords)
+    uint32_t* const wave_lds = lds_tr + (threadIdx.x >> 6) * a.stack_words;
+    S.ring = wave_lds + lane;
     S.stride = a.spill_stride;
     S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
@@ -800,7 +805,7 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
         int32_t htri = -1;
         float ht = kMaxFloat;
         if (kRef) {
-            const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, S.ring, lane, cnt);
+            const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
             htri = h.tri; ht = h.t;
         } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
             trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs, &htri, &ht);
@@ -809,9 +814,14 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
             if (walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
                 while (walk4_step<false>(w, o, d, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs, a.node_mask, cnt)) {
                 }
-                htri = (w.best_id == 0xffffffffu) ? -1 : (int32_t)w.best_id;
                 ht = w.best_t;
-                if (htri >= 0 && !ref_tested(w.best_parent, o, d, w.flags, a.rnodes, a.rparent)) {
+                bool ok = true;
+                if (w.best_slot != kNone) {
+                    const float4 C = a.acc_tris[w.best_slot].c;
+                    htri = (int32_t)__float_as_uint(C.y);
+                    ok = ref_tested(__float_as_uint(C.w), o, d, a.rnodes, a.rparent);
+                }
+                if (!ok) {
                     atomicAdd(a.counters + 8, 1ull);
                     trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
                                &htri, &ht);
@@ -918,7 +928,7 @@ struct pt_ctx {
     uint32_t* pixel_counter = nullptr;
     bool scene_fast = false;
     uint32_t node_mask = 0;
-    uint32_t wf_threshold = 60;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
+    uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     DNode4* nodes4 = nullptr;
@@ -1252,7 +1262,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         Args b = a;
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
-        const size_t lds_wf = (size_t)b.stack_words * 4 * 4 + 4 * sizeof(unsigned long long);
+        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long);
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         const uint32_t need = (a.nunits + 255) / 256;
         if (blocks > need) blocks = need;
@@ -1375,8 +1385,8 @@ extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_o
     a.nodes4 = c->nodes4;
     a.acc_tris = c->acc_tris;
     a.rparent = c->rparent;
-    const uint32_t ring = (uint32_t)(c->depth + 2) > (uint32_t)kRing ? (uint32_t)(c->depth + 2) : (uint32_t)kRing;
-    a.stack_words = ring * 64;
+    a.stack_words = (uint32_t)(c->depth + 2) * 64;
+    if (a.stack_words < (uint32_t)kWaveLdsWords) a.stack_words = kWaveLdsWords;
     const size_t lds = (size_t)a.stack_words * 4 * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_trace: BVH depth %d too deep for the LDS stack", c->depth);
     uint32_t blocks = (n + 255) / 256;
