@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-count", action="store_true", help="skip the counting pass (roofline bytes)")
+    ap.add_argument("--sim-shards", type=int, default=1,
+                    help="diagnostic, single process only: render shard 0 of N (one GPU's share at N GPUs)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
@@ -114,6 +116,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    shards = world if world > 1 else max(1, args.sim_shards)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
@@ -135,7 +138,7 @@ def main():
     def step():
         fb.zero_()
         st = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
-                             flags=args.flags, shard_index=rank, shard_count=world, stream_ptr=stream)
+                             flags=args.flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
         if distributed:
             dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
         return st
@@ -146,7 +149,7 @@ def main():
         fb.zero_()
         counts = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces,
                                  integrator=args.integrator, flags=args.flags | pt.PT_FLAG_COUNT,
-                                 shard_index=rank, shard_count=world, stream_ptr=stream)
+                                 shard_index=rank, shard_count=shards, stream_ptr=stream)
     for _ in range(args.warmup):
         step()
     if distributed:
@@ -222,7 +225,8 @@ def main():
                 scene_name, W, H, args.spp, args.bounces, args.integrator),
                 "scene": scene_name, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "integrator": "unidirectional" if args.integrator == 0 else "head", "seed": 1234,
-                "parallelism": "image tiles %dx, RCCL reduce" % world if distributed else "1 GPU"},
+                "parallelism": ("image tiles %dx, RCCL reduce" % world if distributed else
+                                "1 GPU" if shards == 1 else "1 GPU rendering shard 0 of %d (diagnostic)" % shards)},
             "mrays_per_s_traced": round(traced / elapsed / 1e6, 3),
             "mrays_per_s_reference_equiv": round(refrays / elapsed / 1e6, 3),
             "mrays_per_s_nominal": round(samples * (args.bounces + 1) / elapsed / 1e6, 3),

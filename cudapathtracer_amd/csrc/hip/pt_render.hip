@@ -49,7 +49,7 @@ struct Args {
     uint32_t stack_words;           // LDS words per wave
     float cull_rel, cull_abs;
     uint32_t* pixel_counter;        // wavefront kernel: next pixel unit
-    uint32_t nunits;                // ntiles_shard * 64
+    uint32_t nunits;                // work units: npix * chunks
     uint32_t scene_fast;            // all scene coordinates admit the Markstein quotient
     uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
@@ -60,7 +60,12 @@ struct Args {
     uint32_t spill_stride;
     float acc_root[6];
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
-    const uint32_t* pix_states;     // XORWOW v0..v4 of each work unit, word k of unit u at [k*nunits + u]
+    const uint32_t* pix_states;     // XORWOW v0..v4, d of each work unit, word k of unit u at [k*nunits + u]
+    uint32_t npix;                  // pixel slots of this shard (ntiles_shard * 64)
+    uint32_t chunks;                // sample chunks per pixel: unit u = chunk u / npix of slot u % npix
+    uint32_t* pmemo;                // chunks > 1: primary hit of pixel slot q: [2q] = tri + 2 (0 = not yet), [2q+1] = t
+    double* lbuf;                   // chunks > 1: per-sample radiance, channel k of sample n of pixel slot q
+                                    // at lbuf[(k * spp + n-1) * npix + q]
 };
 
 // ------------------------------------------------------------------ per-lane tracer
@@ -463,9 +468,13 @@ enum : int {
     CW_M = 13,                        // m0..m2 (f64, lo/hi words)
     CW_ACC = 19,                      // acc (f64 x 3)
     CW_WGT = 25,                      // wgt (f64 x 3)
-    kColdWords = 31
+    CW_NEND = 31,                     // last sample number of the unit
+    CW_Q = 32,                        // pixel slot of the unit (per-sample buffer row)
+    kColdWords = 33
 };
-enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4 };
+// CF_OWNER: chunk 0 of a split pixel (publishes its primary hit in pmemo); CF_SHARE: a later
+// chunk (takes the published hit instead of tracing the camera ray again)
+enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16 };
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the word
 // offset k * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -495,27 +504,89 @@ struct ColdRec {
 // kMinWaves: waves per SIMD the register allocation must allow (launch bound); 4 = 128 VGPRs,
 // 5 = 96, 6 = 80 -- more resident waves hide more memory latency, at the price of spilling
 // shading-phase values (the walk loop itself stays spill-free down to 96).
-// setupCurand (kernel.cu:527-533) for the wavefront kernel: the XORWOW state of every work unit
-// (pixel) of this shard, computed in parallel before the render so that a lane starting a pixel
-// inside the state machine loads 20 B instead of running the jump-ahead with its wave waiting.
-__global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __restrict__ st)
+// Work unit u = sample chunk c = u / npix of pixel slot q = u % npix: samples
+// [c*spp/chunks, (c+1)*spp/chunks).  With one chunk a unit is a whole pixel.
+__device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c)
 {
-    const uint32_t u = blockIdx.x * 256u + threadIdx.x;
-    if (u >= a.nunits) return;
-    const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
-    const uint32_t l = u & 63u;
+    return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / a.chunks);
+}
+__device__ __forceinline__ bool unit_pixel(const Args& a, uint32_t q, uint32_t* px, uint32_t* py)
+{
+    const uint32_t t = (uint32_t)a.shard_index + (q >> 6) * (uint32_t)a.shard_count;
+    const uint32_t l = q & 63u;
     const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
     const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
-    const uint32_t px = (t % a.tiles_x) * kTile + qx;
-    const uint32_t py = (t / a.tiles_x) * kTile + qy;
-    if (px >= (uint32_t)a.w || py >= (uint32_t)a.h) return;
+    *px = (t % a.tiles_x) * kTile + qx;
+    *py = (t / a.tiles_x) * kTile + qy;
+    return *px < (uint32_t)a.w && *py < (uint32_t)a.h;
+}
+
+// The XORWOW draws one sample of radianceAlongSingleStep2 consumes, without tracing: the count
+// depends only on the draws themselves (lens pair; per bounce u, then 2 for a cosine direction or
+// 3 for a light sample, which also jumps i to D-2) -- the same replay as the dead-path skip.
+__device__ __forceinline__ void replay_sample(Rng& rng, bool lens, int D)
+{
+    if (lens) { rng_next(rng); rng_next(rng); }
+    int i = 0;
+    while (i < D) {
+        const float u = rng_uniform(rng);
+        if (u < 0.5) { rng_next(rng); rng_next(rng); }
+        else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
+        ++i;
+    }
+}
+
+// setupCurand (kernel.cu:527-533) for the wavefront kernel: the XORWOW state of every work unit
+// of this shard -- curand_init of its pixel, fast-forwarded over the unit's earlier samples --
+// computed in parallel before the render, so that a lane starting a unit inside the state
+// machine loads 20 B instead of running the jump-ahead with its wave waiting.
+__global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __restrict__ st)
+{
+    // one lane per pixel slot: curand_init, then one pass over the samples that writes the state
+    // at the start of every chunk
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= a.npix) return;
+    uint32_t px, py;
+    if (!unit_pixel(a, q, &px, &py)) return;
+    const uint32_t idx = morton2(px, py);
     Rng r;
-    rng_init(r, a.seed, morton2(px, py), a.jump);
-    st[u] = r.v0;
-    st[(size_t)a.nunits + u] = r.v1;
-    st[2 * (size_t)a.nunits + u] = r.v2;
-    st[3 * (size_t)a.nunits + u] = r.v3;
-    st[4 * (size_t)a.nunits + u] = r.v4;
+    rng_init(r, a.seed, idx, a.jump);
+    const bool lens = (idx == 0) || (a.cam.radius != 0.0f);
+    uint32_t done = 0;
+    for (uint32_t c = 0; c < a.chunks; ++c) {
+        for (const uint32_t s0 = chunk_first(a, c); done < s0; ++done) replay_sample(r, lens, a.bounces);
+        const size_t u = (size_t)c * a.npix + q;
+        st[u] = r.v0;
+        st[(size_t)a.nunits + u] = r.v1;
+        st[2 * (size_t)a.nunits + u] = r.v2;
+        st[3 * (size_t)a.nunits + u] = r.v3;
+        st[4 * (size_t)a.nunits + u] = r.v4;
+        st[5 * (size_t)a.nunits + u] = r.d;       // the Weyl counter advances with every draw
+    }
+}
+
+// chunks > 1: the running mean of kernel.cu:551-552, in sample order, over the stored
+// per-sample radiance of each pixel of this shard.
+__global__ __launch_bounds__(256) void finalize_pixels(Args a)
+{
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= a.npix) return;
+    uint32_t px, py;
+    if (!unit_pixel(a, q, &px, &py)) return;
+    const size_t pix = (size_t)py * (size_t)a.w + px;
+    const size_t ch = (size_t)a.spp * a.npix;   // channel stride
+    const double* L = a.lbuf + q;
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    for (int n = 1; n <= a.spp; ++n, L += a.npix) {
+        const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
+        m0 = (m0 * fn1) / fn + L[0] / fn;
+        m1 = (m1 * fn1) / fn + L[ch] / fn;
+        m2 = (m2 * fn1) / fn + L[2 * ch] / fn;
+    }
+    float* o3 = a.out + pix * 3;
+    o3[0] = (float)m0;
+    o3[1] = (float)m1;
+    o3[2] = (float)m2;
 }
 
 // One event per active lane added to an LDS counter with a single atomic per wave.
@@ -628,6 +699,18 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     fl &= ~CF_PRIMARY; state = ST_SHADE;
                     return true;
                 }
+                if (fl & CF_SHARE) {
+                    // the pixel's chunk 0 may have published the (sample-invariant) primary hit
+                    const uint32_t q = R.ld(CW_Q);
+                    const uint32_t tv = __hip_atomic_load(a.pmemo + 2 * (size_t)q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tv != 0u) {
+                        htri = (int32_t)(tv - 2u);
+                        ht = __uint_as_float(a.pmemo[2 * (size_t)q + 1]);
+                        fl = (fl | CF_PRIMARY) & ~CF_SHARE;   // stores the unit memo on shading
+                        state = ST_SHADE;
+                        return true;
+                    }
+                }
                 fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
                 return begin_trace(ro, rd);
             };
@@ -644,6 +727,13 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 if (fl & CF_PRIMARY) {
                     fl = (fl | CF_HAVE) & ~CF_PRIMARY;
                     R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
+                    if (fl & CF_OWNER) {
+                        const uint32_t q = R.ld(CW_Q);
+                        a.pmemo[2 * (size_t)q + 1] = __float_as_uint(ht);
+                        __hip_atomic_store(a.pmemo + 2 * (size_t)q, (uint32_t)(htri + 2), __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        fl &= ~CF_OWNER;
+                    }
                 }
                 // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
                 {
@@ -684,23 +774,36 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 // advance to the next trace this lane needs
                 for (;;) {
                     if (i >= D) {
-                        const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
-                        const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
-                        const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
-                        const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
                         wave_count(lcnt + 2, lane);
-                        if (n >= a.spp) {
-                            const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
-                            float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
-                            o3[0] = (float)m0;
-                            o3[1] = (float)m1;
-                            o3[2] = (float)m2;
-                            state = ST_IDLE;
-                            break;
+                        const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
+                        if (a.chunks == 1) {
+                            const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
+                            const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
+                            const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
+                            const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
+                            if (n >= a.spp) {
+                                float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+                                o3[0] = (float)m0;
+                                o3[1] = (float)m1;
+                                o3[2] = (float)m2;
+                                state = ST_IDLE;
+                                break;
+                            }
+                            R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
+                        } else {
+                            // split pixel: keep L_n, finalize_pixels forms the ordered mean
+                            const size_t ch = (size_t)a.spp * a.npix;
+                            double* L = a.lbuf + (size_t)(n - 1) * a.npix + R.ld(CW_Q);
+                            L[0] = R.ldd(CW_ACC);
+                            L[ch] = R.ldd(CW_ACC + 2);
+                            L[2 * ch] = R.ldd(CW_ACC + 4);
+                            if ((uint32_t)n >= R.ld(CW_NEND)) {
+                                state = ST_IDLE;
+                                break;
+                            }
                         }
-                        R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
                         ++n;
-                        again = start_sample(R.ld(CW_PX), R.ld(CW_PY));
+                        again = start_sample(px, py);
                         break;
                     }
                     if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
@@ -730,24 +833,24 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     if (u >= a.nunits) {
                         state = ST_DONE;
                     } else {
-                        const uint32_t t = (uint32_t)a.shard_index + (u >> 6) * (uint32_t)a.shard_count;
-                        const uint32_t l = u & 63u;
-                        const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
-                        const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
-                        const uint32_t px = (t % a.tiles_x) * kTile + qx;
-                        const uint32_t py = (t / a.tiles_x) * kTile + qy;
-                        if (px < (uint32_t)a.w && py < (uint32_t)a.h) {
+                        const uint32_t c = u / a.npix, q = u - c * a.npix;
+                        uint32_t px, py;
+                        if (unit_pixel(a, q, &px, &py)) {
                             const uint32_t idx = morton2(px, py);
                             // curand_init's state, computed for every unit by init_pixel_states
-                            rng.d = rng_seed_d(a.seed);
+                            rng.d = a.pix_states[5 * (size_t)a.nunits + u];
                             rng.v0 = a.pix_states[u];
                             rng.v1 = a.pix_states[(size_t)a.nunits + u];
                             rng.v2 = a.pix_states[2 * (size_t)a.nunits + u];
                             rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
                             rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
                             fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
-                            n = 1;
+                            if (a.chunks > 1 && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
+                                fl |= (c == 0) ? CF_OWNER : CF_SHARE;
+                            n = (int)chunk_first(a, c) + 1;
                             R.st(CW_PX, px); R.st(CW_PY, py);
+                            R.st(CW_NEND, chunk_first(a, c + 1));
+                            R.st(CW_Q, q);
                             R.std_(CW_M, 0.0); R.std_(CW_M + 2, 0.0); R.std_(CW_M + 4, 0.0);
                             start_sample(px, py);
                         }
@@ -931,13 +1034,18 @@ struct pt_ctx {
     uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
+    int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
     uint32_t* spill = nullptr;
     size_t spill_words = 0;
-    uint32_t* pix_states = nullptr;   // init_pixel_states output (5 words per work unit)
+    uint32_t* pix_states = nullptr;   // init_pixel_states output (6 words per work unit)
     size_t pix_states_words = 0;
+    double* lbuf = nullptr;           // per-sample radiance of split pixels
+    size_t lbuf_words = 0;
+    uint32_t* pmemo = nullptr;        // per-pixel-slot primary hit shared by a split pixel's chunks
+    size_t pmemo_words = 0;
     float acc_root[6];
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
@@ -1092,6 +1200,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         }
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
     }
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
     std::vector<DNode4> an;
@@ -1186,7 +1295,7 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states};
+                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1264,14 +1373,48 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.node_mask = c->node4_mask;
         const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long);
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
-        const uint32_t need = (a.nunits + 255) / 256;
+        // Work units: whole pixels, unless the shard has too few pixels to keep every resident
+        // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
+        // one pixel's time): then each pixel is split into sample chunks.
+        b.npix = a.ntiles_shard * 64u;
+        const uint64_t lanes = (uint64_t)blocks * 256u;
+        uint32_t chunks = 1;
+        if (c->wf_chunks > 0) chunks = (uint32_t)c->wf_chunks;
+        else if (2 * (uint64_t)b.npix < 5 * lanes) chunks = (uint32_t)((24 * lanes + b.npix - 1) / b.npix);
+        // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~24 units per lane)
+        if (chunks > (uint32_t)p->spp) chunks = (uint32_t)p->spp;
+        if ((uint64_t)b.npix * chunks > 0xffffffffull) chunks = 1;
+        b.chunks = chunks;
+        b.nunits = b.npix * chunks;
+        const uint32_t need = (b.nunits + 255) / 256;
         if (blocks > need) blocks = need;
+        if (chunks > 1) {
+            const size_t lw = (size_t)b.npix * (size_t)p->spp * 3;
+            if (c->lbuf_words < lw) {
+                if (c->lbuf) (void)hipFree(c->lbuf);
+                c->lbuf = nullptr;
+                c->lbuf_words = 0;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->lbuf), lw * sizeof(double)));
+                c->lbuf_words = lw;
+            }
+            b.lbuf = c->lbuf;
+            const size_t mw = (size_t)b.npix * 2;
+            if (c->pmemo_words < mw) {
+                if (c->pmemo) (void)hipFree(c->pmemo);
+                c->pmemo = nullptr;
+                c->pmemo_words = 0;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pmemo), mw * 4));
+                c->pmemo_words = mw;
+            }
+            HIP_TRY(hipMemsetAsync(c->pmemo, 0, mw * 4, stream));
+            b.pmemo = c->pmemo;
+        }
         const size_t per_lane = stack_words_per_lane(c);
         if (int rc = ensure_spill(c, (per_lane + kColdWords) * (size_t)blocks * 256)) return rc;
         b.spill = c->spill;
         b.spill_stride = blocks * 256;
         b.cold = c->spill + per_lane * (size_t)b.spill_stride;
-        const size_t sw = (size_t)5 * a.nunits;
+        const size_t sw = (size_t)6 * b.nunits;
         if (c->pix_states_words < sw) {
             if (c->pix_states) (void)hipFree(c->pix_states);
             c->pix_states = nullptr;
@@ -1280,12 +1423,14 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             c->pix_states_words = sw;
         }
         b.pix_states = c->pix_states;
-        hipLaunchKernelGGL(init_pixel_states, dim3((a.nunits + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
+        hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
         if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        HIP_TRY(hipGetLastError());
+        if (b.chunks > 1) hipLaunchKernelGGL(finalize_pixels, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b);
         HIP_TRY(hipGetLastError());
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
