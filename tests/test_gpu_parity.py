@@ -127,6 +127,29 @@ def test_shards_sum_to_full_render(cb):
         assert tot == st["samples"]
 
 
+@pytest.mark.parametrize("chunks,radius", [("1", 0.0), ("3", 0.0), ("7", 0.05), ("64", 0.0)])
+def test_sample_chunk_units_bit_exact(oracle_mod, monkeypatch, chunks, radius):
+    """Work units = (pixel, sample chunk): the XORWOW state fast-forwarded over earlier samples,
+    per-sample radiance combined in order by finalize_pixels, the primary hit shared by a pixel's
+    chunks.  Chunk counts that do not divide spp (7 of 9 samples: chunks of 1 and 2), more chunks
+    than samples (64 -> capped at spp), lens draws in the replay, and whole-pixel units (1)."""
+    monkeypatch.setenv("PT_WF_CHUNKS", chunks)
+    s = load_scene("cornell_blob")
+    w, h, spp = 24, 16, 9
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=3)
+        parts = np.zeros(img.shape, dtype=np.float64)
+        for k in range(3):
+            part, _ = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=3)
+            parts += part
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 0, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert _bits_equal(parts, img.astype(np.float64)) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+
+
 def test_rmse_and_properties_larger(oracle_mod, cb):
     """North-star tolerance on a subset of a larger render (oracle only on the subset)."""
     s, r = cb
