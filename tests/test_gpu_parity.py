@@ -139,7 +139,7 @@ def test_sample_chunk_units_bit_exact(oracle_mod, monkeypatch, chunks, radius):
     cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
     with pt.Renderer(s, 0) as r:
         img, st = r.render(cam, w, h, spp, bounces=3)
-        parts = np.zeros(img.shape, dtype=np.float64)
+        parts = np.zeros_like(img)
         for k in range(3):
             part, _ = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=3)
             parts += part
