@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libptamd.so")
+# PT_LIB selects an experiment build (tools/build_variants.sh); the default is the in-tree library
+LIB_PATH = os.environ.get("PT_LIB") or os.path.join(_HERE, "libptamd.so")
 
 PT_OK = 0
 PT_E_INVALID, PT_E_IO, PT_E_SCENE, PT_E_BVH_DEPTH, PT_E_HIP, PT_E_NODEV, PT_E_OOM = -1, -2, -3, -4, -5, -6, -7

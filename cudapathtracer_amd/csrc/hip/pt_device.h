@@ -508,8 +508,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const DNode4* nd = nodes + (visit ? w.node : 0u);
     float4 lx = nd->lox, ly = nd->loy, lz = nd->loz, hx = nd->hix, hy = nd->hiy, hz = nd->hiz;
     uint4 ch = nd->child;
-    pin(A); pin(B); pin(C);
-    pin(lx); pin(ly); pin(lz); pin(hx); pin(hy); pin(hz); pin(ch);
+    pin(A); pin(B); pin(C);   // (the node's fields feed unconditional tests: no pin needed)
     if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
         const float t = tri_hit_rec<true>(o, d, A, B, C);
