@@ -21,7 +21,7 @@ PT_FLAG_NO_DEAD_PATH_SKIP = 0x2
 PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
-ABI_VERSION = 2                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
+ABI_VERSION = 3                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -95,6 +95,10 @@ SIGNATURES = {
     "pt_render_device": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.c_void_p,
                                    C.POINTER(Stats)]),
     "pt_trace": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "pt_tonemap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "pt_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pt_write_ppm_codes": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "pt_write_pfm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_destroy": (None, [C.c_void_p]),
 }
 

@@ -137,6 +137,30 @@ def tonemap_u8(c):
     return int(L.lib().pt_tonemap_u8(float(c)))
 
 
+def write_ppm_codes(path, codes):
+    """The reference PPM text from (H, W, 3) int32 tone-map codes (e.g. Renderer.tonemap)."""
+    codes = np.ascontiguousarray(codes, dtype=np.int32)
+    h, w = codes.shape[:2]
+    L.check(L.lib().pt_write_ppm_codes(str(path).encode(), codes.ctypes.data, w, h))
+
+
+def write_pfm(path, img):
+    """Lossless float dump (PFM, little-endian, rows bottom-up) of an (H, W, 3) mean image."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    h, w = img.shape[:2]
+    L.check(L.lib().pt_write_pfm(str(path).encode(), img.ctypes.data, w, h))
+
+
+def read_pfm(path):
+    """Inverse of write_pfm: (H, W, 3) float32."""
+    with open(path, "rb") as fh:
+        assert fh.readline().strip() == b"PF"
+        w, h = (int(v) for v in fh.readline().split())
+        scale = float(fh.readline())
+        data = np.frombuffer(fh.read(), dtype="<f4" if scale < 0 else ">f4")
+    return data.reshape(h, w, 3)[::-1].astype(np.float32)
+
+
 class Renderer:
     """Device-resident scene on one GPU (pt_create) and the render call (pt_render)."""
 
@@ -190,6 +214,15 @@ class Renderer:
         L.check(L.lib().pt_render_device(self._h, C.byref(p), C.byref(cam), C.c_void_p(int(d_out_ptr)),
                                          None if stream_ptr is None else C.c_void_p(int(stream_ptr)), C.byref(st)))
         return st.as_dict()
+
+    def tonemap(self, img):
+        """Output step on the GPU: (H, W, 3) float32 mean image -> int32 codes equal to
+        pt_tonemap_u8 (kernel.cu:763-778) per channel."""
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        h, w = img.shape[:2]
+        codes = np.empty(img.shape, dtype=np.int32)
+        L.check(L.lib().pt_tonemap(self._h, img.ctypes.data, w, h, codes.ctypes.data))
+        return codes
 
     def trace(self, origins, directions, reference_bvh=False):
         """The reference's trace() (kernel.cu:112-161) for a batch of rays: returns

@@ -1,0 +1,182 @@
+// pt_cli -- the reference's program (kernel.cu:565-790 `main`) as a command-line tool over the
+// C-ABI of include/pt/pt.h: load OBJ models (loadOBJ, kernel.cu:589-599), build the BVH
+// (:601, depth guard :627-631), render (:702-737), report rates (:753-757, in 64-bit), tone-map
+// on the GPU and write the PPM (:763-778), optionally a PFM float dump.
+//
+//   pt_cli --obj models/CornellBox-Original.obj --obj models/teapot.obj@0.35,0.6,0.3@0.75 \
+//          --width 512 --height 512 --spp 99 --bounces 3 --out image.ppm [--pfm image.pfm]
+//
+// --obj PATH[@ox,oy,oz[@scale[@flip]]]   loadOBJ(path, mtl dir, origin, scale, flipNormals)
+// --num-samples N                         the reference's NUM_SAMPLES (renders N-1 samples);
+//                                         --spp gives the sample count directly
+// --gpus N                                shard image tiles over devices 0..N-1 (one host thread
+//                                         and context per device; shards are disjoint, summed)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pt/pt.h"
+
+namespace {
+
+struct Obj {
+    std::string path;
+    pt_vec3 origin{0, 0, 0};
+    float scale = 1.0f;
+    int flip = 0;
+};
+
+[[noreturn]] void usage(const char* msg)
+{
+    if (msg) fprintf(stderr, "pt_cli: %s\n", msg);
+    fprintf(stderr,
+            "usage: pt_cli --obj PATH[@ox,oy,oz[@scale[@flip]]] [--obj ...] [--mtl-dir DIR]\n"
+            "              [--width W] [--height H] [--spp N | --num-samples N] [--bounces D]\n"
+            "              [--integrator unidir|head] [--seed S] [--cam X,Y,Z] [--dist D] [--focal F]\n"
+            "              [--radius R] [--gpus N] [--out image.ppm] [--pfm image.pfm] [--quiet]\n");
+    exit(2);
+}
+
+bool parse_vec3(const std::string& s, pt_vec3* v)
+{
+    return sscanf(s.c_str(), "%f,%f,%f", &v->x, &v->y, &v->z) == 3;
+}
+
+Obj parse_obj(const std::string& arg)
+{
+    Obj o;
+    std::vector<std::string> parts;
+    size_t b = 0;
+    for (size_t e; (e = arg.find('@', b)) != std::string::npos; b = e + 1) parts.push_back(arg.substr(b, e - b));
+    parts.push_back(arg.substr(b));
+    o.path = parts[0];
+    if (parts.size() > 1 && !parse_vec3(parts[1], &o.origin)) usage("bad --obj origin");
+    if (parts.size() > 2) o.scale = strtof(parts[2].c_str(), nullptr);
+    if (parts.size() > 3) o.flip = atoi(parts[3].c_str());
+    return o;
+}
+
+std::string dir_of(const std::string& p)
+{
+    const size_t k = p.find_last_of('/');
+    return k == std::string::npos ? std::string("./") : p.substr(0, k + 1);
+}
+
+int die(const char* what)
+{
+    fprintf(stderr, "pt_cli: %s: %s\n", what, pt_last_error());
+    return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    std::vector<Obj> objs;
+    std::string mtl_dir, out = "image.ppm", pfm;
+    pt_params p{};
+    p.width = 512; p.height = 512; p.spp = 99; p.bounces = 3;   // kernel.cu:29-33 defaults
+    p.integrator = PT_INTEGRATOR_UNIDIR; p.seed = 1234; p.shard_index = 0; p.shard_count = 1;
+    pt_camera cam{{0, 1, 3}, 1, 3, 0, 0, 0};                      // kernel.cu:642-648
+    int gpus = 1;
+    bool quiet = false;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto next = [&]() -> std::string {
+            if (i + 1 >= argc) usage(("missing value for " + a).c_str());
+            return argv[++i];
+        };
+        if (a == "--obj") objs.push_back(parse_obj(next()));
+        else if (a == "--mtl-dir") mtl_dir = next();
+        else if (a == "--width") p.width = atoi(next().c_str());
+        else if (a == "--height") p.height = atoi(next().c_str());
+        else if (a == "--spp") p.spp = atoi(next().c_str());
+        else if (a == "--num-samples") p.spp = atoi(next().c_str()) - 1;   // kernel.cu:709-710
+        else if (a == "--bounces") p.bounces = atoi(next().c_str());
+        else if (a == "--integrator") {
+            const std::string v = next();
+            if (v == "unidir") p.integrator = PT_INTEGRATOR_UNIDIR;
+            else if (v == "head") p.integrator = PT_INTEGRATOR_HEAD;
+            else usage("--integrator is unidir or head");
+        } else if (a == "--seed") p.seed = strtoull(next().c_str(), nullptr, 10);
+        else if (a == "--cam") { if (!parse_vec3(next(), &cam.pos)) usage("bad --cam"); }
+        else if (a == "--dist") cam.dist_from_film = strtof(next().c_str(), nullptr);
+        else if (a == "--focal") cam.focal_length = strtof(next().c_str(), nullptr);
+        else if (a == "--radius") cam.radius = strtof(next().c_str(), nullptr);
+        else if (a == "--gpus") gpus = atoi(next().c_str());
+        else if (a == "--out") out = next();
+        else if (a == "--pfm") pfm = next();
+        else if (a == "--quiet") quiet = true;
+        else if (a == "-h" || a == "--help") usage(nullptr);
+        else usage(("unknown option " + a).c_str());
+    }
+    if (objs.empty()) usage("at least one --obj is required");
+    if (gpus < 1) usage("--gpus must be >= 1");
+    cam.pxl_width = p.width;
+    cam.pxl_height = p.height;
+
+    const auto t0 = std::chrono::steady_clock::now();
+    pt_host_scene* s = pt_scene_new();
+    for (const Obj& o : objs) {
+        const std::string md = mtl_dir.empty() ? dir_of(o.path) : mtl_dir;
+        if (pt_scene_load_obj(s, o.path.c_str(), md.c_str(), o.origin, o.scale, o.flip) != PT_OK) return die("loadOBJ");
+        const char* warn = pt_scene_last_warning(s);
+        if (warn && *warn && !quiet) fprintf(stderr, "%s", warn);
+    }
+    if (pt_scene_build_bvh(s) != PT_OK) return die("buildBVH");
+    pt_scene view;
+    pt_scene_view(s, &view);
+    const double t_load = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!quiet)
+        printf("scene: %u triangles, %u lights, BVH depth %d (load + build %.3f s)\n", view.num_tris, view.num_lights,
+               view.bvh_depth, t_load);
+
+    const size_t n = (size_t)p.width * p.height * 3;
+    std::vector<pt_ctx*> ctx(gpus, nullptr);
+    for (int g = 0; g < gpus; ++g) {
+        int err = 0;
+        ctx[g] = pt_create(&view, g, &err);
+        if (!ctx[g]) return die("pt_create");
+    }
+    std::vector<std::vector<float>> part(gpus, std::vector<float>(n));
+    std::vector<pt_stats> st(gpus);
+    std::vector<int> rc(gpus, PT_OK);
+    std::vector<std::thread> th;
+    const auto t1 = std::chrono::steady_clock::now();
+    for (int g = 0; g < gpus; ++g)
+        th.emplace_back([&, g]() {
+            pt_params q = p;
+            q.shard_index = g;
+            q.shard_count = gpus;
+            rc[g] = pt_render(ctx[g], &q, &cam, part[g].data(), &st[g]);
+        });
+    for (std::thread& t : th) t.join();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    for (int g = 0; g < gpus; ++g)
+        if (rc[g] != PT_OK) return die("pt_render");
+    std::vector<float> img(n, 0.0f);
+    uint64_t samples = 0, traced = 0, reference = 0, nominal = 0;
+    for (int g = 0; g < gpus; ++g) {
+        for (size_t k = 0; k < n; ++k) img[k] += part[g][k];   // disjoint shards: x + 0 = x
+        samples += st[g].samples;
+        traced += st[g].rays_traced;
+        reference += st[g].rays_reference;
+        nominal = st[g].rays_nominal;
+    }
+    if (!quiet) {
+        printf("%d GPU(s): %.3f s, %.1f Msamples/s, %.1f Mrays/s traced, %.1f Mrays/s reference-equivalent, "
+               "%.1f Mrays/s nominal (kernel.cu:757)\n",
+               gpus, secs, samples / secs / 1e6, traced / secs / 1e6, reference / secs / 1e6, nominal / secs / 1e6);
+    }
+    std::vector<int32_t> codes(n);
+    if (pt_tonemap(ctx[0], img.data(), p.width, p.height, codes.data()) != PT_OK) return die("tone map");
+    if (pt_write_ppm_codes(out.c_str(), codes.data(), p.width, p.height) != PT_OK) return die("write PPM");
+    if (!pfm.empty() && pt_write_pfm(pfm.c_str(), img.data(), p.width, p.height) != PT_OK) return die("write PFM");
+    for (pt_ctx* c : ctx) pt_destroy(c);
+    pt_scene_free(s);
+    return 0;
+}

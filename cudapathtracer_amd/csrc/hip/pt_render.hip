@@ -884,6 +884,35 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     }
 }
 
+// ------------------------------------------------------------------ output step
+// kernel.cu:763-778 / color.h:59-71 on the GPU: code = (int)(pow(c/(c+1), (float)(1/2.2))*255)
+// per channel, read off a table of the 255 boundaries the HOST's libm puts between codes
+// (pt::tonemap_thresholds), so the codes equal pt_tonemap_u8 exactly.
+__global__ __launch_bounds__(256) void tonemap_codes(const float* __restrict__ rgb, size_t n,
+                                                     const float* __restrict__ thr, int32_t* __restrict__ out)
+{
+    __shared__ float t[256];
+    t[threadIdx.x] = thr[threadIdx.x];
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float c = rgb[i];
+        int32_t code;
+        if (!(c == c) || c == INFINITY) {
+            code = INT32_MIN;                // c/(c+1) is NaN: (int)NaN on x86
+        } else if (c < 0.0f) {
+            code = INT32_MAX;                // never produced by the integrator; redone on the host
+        } else {
+            int lo = 0, hi = 255;            // largest k with t[k] <= c (t[0] = 0)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (t[mid] <= c) lo = mid; else hi = mid - 1;
+            }
+            code = lo;
+        }
+        out[i] = code;
+    }
+}
+
 // ------------------------------------------------------------------ batched trace()
 // pt_trace: the reference's trace() (kernel.cu:112-161) for a batch of rays, one lane per ray,
 // on the same walk the wavefront kernel uses (BVH4 + winner check + exact slow path), or on the
@@ -1046,6 +1075,8 @@ struct pt_ctx {
     size_t lbuf_words = 0;
     uint32_t* pmemo = nullptr;        // per-pixel-slot primary hit shared by a split pixel's chunks
     size_t pmemo_words = 0;
+    float* tone_thr = nullptr;        // output step: the host libm's 255 code boundaries (+ t[0] = 0)
+    bool tone_ok = false;
     float acc_root[6];
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
@@ -1269,11 +1300,13 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     std::vector<uint32_t> jump_img, jump;
     build_jump_tables(jump_img);
     build_jump_bytes(jump_img, jump);
+    std::vector<float> tone(256);
+    c->tone_ok = pt::tonemap_thresholds(tone.data());
 
     int rc = PT_OK;
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
-        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) ||
+        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) ||
         (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar))) {
         pt_destroy(c);
         return bail(rc);
@@ -1295,7 +1328,8 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo};
+                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
+                    c->tone_thr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1563,5 +1597,45 @@ extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_o
     if (d_rays) (void)hipFree(d_rays);
     if (d_tri) (void)hipFree(d_tri);
     if (d_t) (void)hipFree(d_t);
+    return rc;
+}
+
+extern "C" int pt_tonemap_device(pt_ctx* c, const float* d_rgb, int w, int h, int32_t* d_codes, void* stream_v)
+{
+    pt::clear_error();
+    if (!c || !d_rgb || !d_codes || w <= 0 || h <= 0) return pt::fail(PT_E_INVALID, "pt_tonemap_device: bad arguments");
+    if (!c->tone_ok) return pt::fail(PT_E_INVALID, "pt_tonemap_device: host tone map not monotone; use pt_tonemap_u8");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+    const size_t n = (size_t)w * (size_t)h * 3;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > (size_t)c->num_cus * 32) blocks = (size_t)c->num_cus * 32;
+    hipLaunchKernelGGL(tonemap_codes, dim3((unsigned)blocks), dim3(256), 0, stream, d_rgb, n, c->tone_thr, d_codes);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(stream));
+    return PT_OK;
+}
+
+extern "C" int pt_tonemap(pt_ctx* c, const float* rgb, int w, int h, int32_t* codes)
+{
+    pt::clear_error();
+    if (!c || !rgb || !codes || w <= 0 || h <= 0) return pt::fail(PT_E_INVALID, "pt_tonemap: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = (size_t)w * (size_t)h * 3;
+    float* d_rgb = nullptr;
+    int32_t* d_codes = nullptr;
+    auto run = [&]() -> int {
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_rgb), n * sizeof(float)));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_codes), n * sizeof(int32_t)));
+        HIP_TRY(hipMemcpy(d_rgb, rgb, n * sizeof(float), hipMemcpyHostToDevice));
+        if (int rc = pt_tonemap_device(c, d_rgb, w, h, d_codes, nullptr)) return rc;
+        HIP_TRY(hipMemcpy(codes, d_codes, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i)
+            if (codes[i] == INT32_MAX) codes[i] = pt_tonemap_u8((double)rgb[i]);
+        return PT_OK;
+    };
+    const int rc = run();
+    if (d_rgb) (void)hipFree(d_rgb);
+    if (d_codes) (void)hipFree(d_codes);
     return rc;
 }

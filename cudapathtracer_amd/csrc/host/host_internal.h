@@ -60,6 +60,7 @@ struct HostScene {
 
 // Deterministic float sin/cos shared with the kernels (defined in hip/pt_render.hip).
 void sincos_det(float theta, float* s, float* c);
+bool tonemap_thresholds(float t[256]);
 
 // ---- render-path acceleration structure (accel_build.cpp) --------------------------------
 struct AccelNode {

@@ -230,6 +230,70 @@ extern "C" int pt_write_ppm(const char* path, const float* rgb, int width, int h
     return write_ppm_any(path, rgb, width, height);
 }
 
+// The reference's PPM text (kernel.cu:763-778) from tone-mapped codes (pt_tonemap / GPU).
+extern "C" int pt_write_ppm_codes(const char* path, const int32_t* codes, int w, int h)
+{
+    if (!path || !codes || w <= 0 || h <= 0) return fail(PT_E_INVALID, "pt_write_ppm_codes: bad arguments");
+    FILE* fp = fopen(path, "w");
+    if (!fp) return fail(PT_E_IO, "pt_write_ppm_codes: cannot open %s", path);
+    fprintf(fp, "P3 %d %d 255\n", w, h);
+    for (int y = 0; y < h; ++y)
+        for (int x = w - 1; x >= 0; --x) {                                         // mirrored, kernel.cu:766
+            const int32_t* p = codes + (static_cast<size_t>(y) * w + x) * 3;
+            fprintf(fp, "%d %d %d ", p[0], p[1], p[2]);
+        }
+    if (fclose(fp) != 0) return fail(PT_E_IO, "pt_write_ppm_codes: write failed for %s", path);
+    return PT_OK;
+}
+
+// Portable float map of the fp32 mean image (little-endian, scale -1, rows bottom-up per the
+// PFM convention): the lossless dump for parity checks.
+extern "C" int pt_write_pfm(const char* path, const float* rgb, int w, int h)
+{
+    if (!path || !rgb || w <= 0 || h <= 0) return fail(PT_E_INVALID, "pt_write_pfm: bad arguments");
+    FILE* fp = fopen(path, "wb");
+    if (!fp) return fail(PT_E_IO, "pt_write_pfm: cannot open %s", path);
+    fprintf(fp, "PF\n%d %d\n-1.0\n", w, h);
+    bool ok = true;
+    for (int y = h - 1; y >= 0 && ok; --y)
+        ok = fwrite(rgb + static_cast<size_t>(y) * w * 3, sizeof(float), static_cast<size_t>(w) * 3, fp) ==
+             static_cast<size_t>(w) * 3;
+    if (fclose(fp) != 0 || !ok) return fail(PT_E_IO, "pt_write_pfm: write failed for %s", path);
+    return PT_OK;
+}
+
+namespace pt {
+// Tone-map thresholds for the GPU output step: t[k] (k = 1..255) = the smallest non-negative
+// float c with pt_tonemap_u8(c) >= k.  The map is monotone in c (c/(c+1), pow, *255 and the
+// truncation all are), so for finite c >= 0 the code is the number of thresholds <= c, exactly
+// as this host's libm computes it.  t[0] = 0.  Returns false if a bisection finds the map
+// non-monotone at a boundary (then the device step must not be used).
+bool tonemap_thresholds(float t[256])
+{
+    t[0] = 0.0f;
+    bool ok = true;
+    for (int k = 1; k < 256; ++k) {
+        uint32_t lo = 0, hi = 0x7f7fffffu;   // [0, FLT_MAX]; f(FLT_MAX) = 255
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            float c;
+            memcpy(&c, &mid, 4);
+            if (pt_tonemap_u8(static_cast<double>(c)) >= k) hi = mid; else lo = mid + 1;
+        }
+        memcpy(&t[k], &lo, 4);
+        if (pt_tonemap_u8(static_cast<double>(t[k])) < k) ok = false;
+        if (lo > 0) {
+            float below;
+            const uint32_t b = lo - 1;
+            memcpy(&below, &b, 4);
+            if (pt_tonemap_u8(static_cast<double>(below)) >= k) ok = false;
+        }
+        if (k > 1 && t[k] < t[k - 1]) ok = false;
+    }
+    return ok;
+}
+}  // namespace pt
+
 extern "C" int pt_write_ppm_f64(const char* path, const double* rgb, int width, int height)
 {
     return write_ppm_any(path, rgb, width, height);

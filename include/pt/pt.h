@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 /* ---- status codes */
 #define PT_OK 0
@@ -114,6 +114,12 @@ int pt_write_ppm_f64(const char* path, const double* rgb, int width, int height)
 /* PPM tone map of one value: (int)(pow(c/(c+1), (double)(float)(1/2.2)) * 255). */
 int pt_tonemap_u8(double c);
 
+/* The PPM text of kernel.cu:763-778 from already tone-mapped codes codes[(y*W+x)*3+k] (the
+ * values pt_tonemap_u8 / pt_tonemap produce), and a PFM float dump of the fp32 mean image
+ * (lossless; rows bottom-up, little-endian, per the PFM format). */
+int pt_write_ppm_codes(const char* path, const int32_t* codes, int width, int height);
+int pt_write_pfm(const char* path, const float* rgb, int width, int height);
+
 /* ============================================================================ render */
 typedef struct pt_ctx pt_ctx;
 
@@ -180,6 +186,14 @@ int pt_render_device(pt_ctx* ctx, const pt_params* params, const pt_camera* cam,
  * (MAX_FLOAT = 1e5 on a miss).  flags: 0 = the render path's walk, PT_FLAG_REFERENCE_BVH = the
  * reference's own stack walk on its BVH.  Bit-identical to the reference for both.  Blocking. */
 int pt_trace(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags);
+
+/* Output step on the GPU (kernel.cu:763-778, color.h:59-71): codes = pt_tonemap_u8(rgb) per
+ * channel, identical to the host function (threshold table bisected with the host's libm at
+ * pt_create).  _device: device pointers on `stream`, blocking; negative inputs (which the
+ * integrator never produces) are written as INT32_MAX for the caller to redo on the host.
+ * pt_tonemap: host buffers, negatives handled. */
+int pt_tonemap_device(pt_ctx* ctx, const float* d_rgb, int width, int height, int32_t* d_codes, void* stream);
+int pt_tonemap(pt_ctx* ctx, const float* rgb, int width, int height, int32_t* codes);
 
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(void);

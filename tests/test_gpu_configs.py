@@ -1,0 +1,96 @@
+"""SURVEY 8 configs at their full sizes on one MI355X.  The whole image is rendered on the GPU;
+the oracle (CPU, test infrastructure) recomputes a spread subset of pixels at full spp and
+depth, which must match bit-for-bit; the rest is checked through properties (finite,
+non-negative, sample counts, shard disjointness).
+
+C2  Cornell mesh 1024x1024, 64 spp, depth 8
+C3  262K-triangle stand-in 1920x1080, 256 spp, depth 3 (the bench workload)
+C4  same at 1024 spp, one GPU's shard of 8 (sample-chunk work units at scale)
+C5  stand-in 3840x2160, 4096 spp, depth 16
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_scene
+
+import cudapathtracer_amd as pt
+from cudapathtracer_amd import scenes, shard
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def standin(tmp_path_factory):
+    d = tmp_path_factory.mktemp("standin")
+    p = scenes.write_sponza_standin(str(d))
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    s.build_bvh()
+    r = pt.Renderer(s, 0)
+    yield s, r
+    r.close()
+
+
+def _check(scene, img, cam_kw, w, h, spp, bounces, pixels):
+    import oracle
+    osc = oracle.OracleScene(scene.arrays())
+    ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"], w, h)
+    ref, _ = oracle.render(osc, ocam, w, h, spp, bounces, 0, 1234, pixels=pixels)
+    a = img.reshape(-1, 3)[pixels]
+    b = ref.reshape(-1, 3)[pixels].astype(np.float32)
+    bad = np.nonzero(np.any(a.view(np.uint32) != b.view(np.uint32), axis=1))[0]
+    assert len(bad) == 0, (len(bad), [int(pixels[i]) for i in bad[:5]])
+
+
+def _spread(w, h, n, seed):
+    rng = np.random.default_rng(seed)
+    pix = rng.choice(w * h, size=n, replace=False).astype(np.uint32)
+    return np.unique(np.concatenate([pix, [0, w * h - 1]]).astype(np.uint32))
+
+
+def test_c2_cornell_1024_64spp_depth8():
+    s = load_scene("cornell")
+    w = h = 1024
+    cam_kw = scenes.CORNELL_CAMERA
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 64, bounces=8)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    assert st["samples"] == w * h * 64
+    _check(s, img, cam_kw, w, h, 64, 8, _spread(w, h, 48, 1))
+
+
+def test_c3_standin_1080p_256spp(standin):
+    s, r = standin
+    w, h = 1920, 1080
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 256, bounces=3)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    assert st["samples"] == w * h * 256
+    _check(s, img, cam_kw, w, h, 256, 3, _spread(w, h, 24, 2))
+
+
+def test_c4_standin_1080p_1024spp_shard_of_8(standin):
+    s, r = standin
+    w, h = 1920, 1080
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 1024, bounces=3,
+                       shard_index=3, shard_count=8)
+    mine = shard.shard_pixels(w, h, 3, 8)
+    mask = np.zeros(w * h, dtype=bool)
+    mask[mine] = True
+    assert np.all(img.reshape(-1, 3)[~mask] == 0)
+    assert st["samples"] == len(mine) * 1024
+    rng = np.random.default_rng(3)
+    _check(s, img, cam_kw, w, h, 1024, 3, np.unique(rng.choice(mine, 12, replace=False)).astype(np.uint32))
+
+
+def test_c5_standin_4k_4096spp_depth16(standin):
+    s, r = standin
+    w, h = 3840, 2160
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 4096, bounces=16)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    assert st["samples"] == w * h * 4096
+    _check(s, img, cam_kw, w, h, 4096, 16, _spread(w, h, 6, 4))

@@ -185,3 +185,23 @@ def test_culled_walk_agrees_with_reference_walk_standin(tmp_path):
     assert sa["rays_reference"] == sb["rays_reference"] == sc["rays_reference"]
     # the SAH walk's winners are checked against the reference BVH; re-walks must be rare
     assert sa["accel_fallbacks"] <= max(10, sa["rays_traced"] // 10000)
+
+
+def test_gpu_output_step_equals_host_tonemap(cb, tmp_path):
+    """pt_tonemap (GPU threshold table) == pt_tonemap_u8 (host libm) on a render and on edge
+    values (0, -0, subnormal, FLT_MAX, inf, NaN, negatives redone on the host); the PPM written
+    from GPU codes is byte-identical to the host writer's."""
+    s, r = cb
+    w, h = 40, 24
+    img, _ = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, 3)
+    codes = r.tonemap(img)
+    ref = np.vectorize(pt.tonemap_u8)(img.astype(np.float64))
+    assert np.array_equal(codes, ref)
+    a, b = str(tmp_path / "a.ppm"), str(tmp_path / "b.ppm")
+    pt.write_ppm(a, img)
+    pt.write_ppm_codes(b, codes)
+    assert open(a, "rb").read() == open(b, "rb").read()
+    edge = np.array([0.0, -0.0, 1e-45, 1e-38, 3.4028235e38, np.inf, np.nan, -0.5, -1.0, -2.0, 1.0, 0.25],
+                    dtype=np.float32)
+    e = np.resize(edge, (1, 4, 3))
+    assert np.array_equal(r.tonemap(e), np.vectorize(pt.tonemap_u8)(e.astype(np.float64)))

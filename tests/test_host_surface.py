@@ -143,3 +143,47 @@ def test_tonemap_and_ppm_match_reference(tmp_path):
 
 def test_structs_match_reference_layouts():
     assert api.VEC3.itemsize == 12 and api.TRI.itemsize == 28 and api.MAT.itemsize == 48 and api.NODE.itemsize == 32
+
+
+def test_ppm_from_codes_and_pfm_roundtrip(tmp_path):
+    """pt_write_ppm_codes(pt_tonemap_u8(img)) is byte-identical to pt_write_ppm(img); the PFM
+    dump round-trips every float bit."""
+    rng = np.random.default_rng(4)
+    img = (rng.exponential(0.3, size=(7, 11, 3))).astype(np.float32)
+    img[0, 0] = [0.0, np.float32(1e-30), np.float32(3e38)]
+    a, b, c = (str(tmp_path / n) for n in ("a.ppm", "b.ppm", "c.pfm"))
+    pt.write_ppm(a, img)
+    codes = np.vectorize(pt.tonemap_u8)(img.astype(np.float64)).astype(np.int32)
+    pt.write_ppm_codes(b, codes)
+    assert open(a, "rb").read() == open(b, "rb").read()
+    pt.write_pfm(c, img)
+    back = pt.read_pfm(c)
+    assert back.tobytes() == img.tobytes()
+
+
+def _tone_thresholds():
+    t = [0.0]
+    for k in range(1, 256):
+        lo, hi = 0, 0x7F7FFFFF
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if pt.tonemap_u8(float(np.uint32(mid).view(np.float32))) >= k:
+                hi = mid
+            else:
+                lo = mid + 1
+        t.append(float(np.uint32(lo).view(np.float32)))
+    return np.array(t, dtype=np.float32)
+
+
+def test_tonemap_threshold_table_reproduces_host_function():
+    """The GPU output step's premise: for finite c >= 0 the code is the number of host-libm
+    bisected thresholds <= c (monotone map).  Checked at every threshold, one float below it,
+    and on 200K random floats across [0, 1e6]."""
+    t = _tone_thresholds()
+    assert np.all(np.diff(t) >= 0)
+    below = (t[1:].view(np.uint32) - 1).view(np.float32)
+    probe = np.concatenate([t, below, np.random.default_rng(5).uniform(0, 1, 100000).astype(np.float32),
+                            np.exp(np.random.default_rng(6).uniform(-30, 14, 100000)).astype(np.float32)])
+    got = np.searchsorted(t[1:], probe, side="right")
+    ref = np.array([pt.tonemap_u8(float(c)) for c in probe])
+    assert np.array_equal(got, ref)
