@@ -90,6 +90,8 @@ SIGNATURES = {
     "pt_write_ppm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_write_ppm_f64": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_tonemap_u8": (C.c_int, [C.c_double]),
+    "pt_accel_digest": (C.c_int, [C.POINTER(SceneView), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                  C.POINTER(C.c_int32)]),
     "pt_create": (C.c_void_p, [C.POINTER(SceneView), C.c_int, C.POINTER(C.c_int)]),
     "pt_render": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.POINTER(Stats)]),
     "pt_render_device": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.c_void_p,

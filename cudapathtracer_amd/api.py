@@ -80,6 +80,14 @@ class Scene:
         L.check(L.lib().pt_scene_view(self._h, C.byref(v)))
         return v
 
+    def accel_digest(self):
+        """(digest, BVH4 node count, BVH4 depth) of the render path's acceleration structure
+        as pt_create would build it (host-only diagnostic)."""
+        v = self.view()
+        dg, n4, d4 = C.c_uint64(), C.c_uint32(), C.c_int32()
+        L.check(L.lib().pt_accel_digest(C.byref(v), C.byref(dg), C.byref(n4), C.byref(d4)))
+        return int(dg.value), int(n4.value), int(d4.value)
+
     def arrays(self):
         """Copies of verts/tris/mats/lights/bvh as numpy structured arrays (test surface)."""
         v = self.view()

@@ -1091,6 +1091,15 @@ extern "C" {
 
 pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
 {
+    // PT_TIMING=1: host-side phase times on stderr (ingest-speed measurements)
+    const bool timing = getenv("PT_TIMING") != nullptr;
+    auto tstart = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "pt_create: %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tstart).count());
+        tstart = now;
+    };
     auto bail = [&](int code) -> pt_ctx* { if (err) *err = code; return nullptr; };
     if (!sc || !sc->verts || !sc->tris || !sc->mats || !sc->bvh) return bail(pt::fail(PT_E_INVALID, "pt_create: incomplete scene"));
     if (sc->num_tris < 2 || sc->bvh_size != sc->num_tris - 1)
@@ -1117,6 +1126,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     for (uint32_t j = 0; j < sc->num_lights; ++j)
         if (sc->lights[j] >= nt) return bail(pt::fail(PT_E_SCENE, "pt_create: light %u indexes triangle %u", j, sc->lights[j]));
     // validate the BVH: every reference must be in range, every triangle reachable once
+    lap("device query");
     std::vector<uint32_t> leaf_rank(nt, 0xffffffffu);
     std::vector<uint32_t> leaf_order;
     leaf_order.reserve(nt);
@@ -1239,8 +1249,11 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     {
         pt::AccelBvh acc;
         pt::Accel4 acc4;
+        lap("reference-BVH records");
         int rc4 = pt::build_accel(*sc, &acc);
+        lap("SAH BVH build");
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
+        lap("BVH4 collapse");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }
         an.resize(acc4.nodes.size());
         for (size_t i = 0; i < acc4.nodes.size(); ++i) {
@@ -1304,6 +1317,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     c->tone_ok = pt::tonemap_thresholds(tone.data());
 
     int rc = PT_OK;
+    lap("records + jump/tone tables");
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) ||
@@ -1319,6 +1333,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
     }
     if (err) *err = PT_OK;
+    lap("uploads");
     return c;
 }
 

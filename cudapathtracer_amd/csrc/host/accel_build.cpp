@@ -10,8 +10,10 @@
 // and nested boxes, the parent test implies every ancestor test).  Boxes are inflated by a
 // margin far above the slab arithmetic's rounding so the culling stays conservative.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
+#include <thread>
 
 #include "host_internal.h"
 
@@ -50,90 +52,169 @@ struct Builder {
         }
     }
 
-    // Returns the child reference of the subtree over items[b, e).
+    // 32-bin SAH split of items[b, e) (n > 1): partitions in place, returns the split point
+    size_t split(size_t b, size_t e) const
+    {
+        const size_t n = e - b;
+        size_t mid = b + n / 2;
+        if (n <= 2) return mid;
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t i = b; i < e; ++i)
+            for (int k = 0; k < 3; ++k) {
+                clo[k] = std::min(clo[k], tb[items[i]].c[k]);
+                chi[k] = std::max(chi[k], tb[items[i]].c[k]);
+            }
+        constexpr int kBins = 32;
+        float best_cost = INFINITY;
+        int best_axis = -1, best_split = 0;
+        for (int k = 0; k < 3; ++k) {
+            const float ext = chi[k] - clo[k];
+            if (!(ext > 0.0f)) continue;
+            int cnt[kBins] = {0};
+            float blo[kBins][3], bhi[kBins][3];
+            for (int q = 0; q < kBins; ++q)
+                for (int j = 0; j < 3; ++j) { blo[q][j] = INFINITY; bhi[q][j] = -INFINITY; }
+            const float scale = kBins / ext;
+            for (size_t i = b; i < e; ++i) {
+                const TriBox& t = tb[items[i]];
+                int q = static_cast<int>((t.c[k] - clo[k]) * scale);
+                q = std::min(kBins - 1, std::max(0, q));
+                ++cnt[q];
+                for (int j = 0; j < 3; ++j) { blo[q][j] = std::min(blo[q][j], t.lo[j]); bhi[q][j] = std::max(bhi[q][j], t.hi[j]); }
+            }
+            float rlo[kBins][3], rhi[kBins][3];
+            int rc[kBins];
+            float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int ac = 0;
+            for (int q = kBins - 1; q >= 0; --q) {
+                for (int j = 0; j < 3; ++j) { alo[j] = std::min(alo[j], blo[q][j]); ahi[j] = std::max(ahi[j], bhi[q][j]); }
+                ac += cnt[q];
+                memcpy(rlo[q], alo, sizeof(alo));
+                memcpy(rhi[q], ahi, sizeof(ahi));
+                rc[q] = ac;
+            }
+            float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int lc = 0;
+            for (int q = 0; q < kBins - 1; ++q) {
+                for (int j = 0; j < 3; ++j) { llo[j] = std::min(llo[j], blo[q][j]); lhi[j] = std::max(lhi[j], bhi[q][j]); }
+                lc += cnt[q];
+                if (lc == 0 || rc[q + 1] == 0) continue;
+                const float cost = lc * surface(llo, lhi) + rc[q + 1] * surface(rlo[q + 1], rhi[q + 1]);
+                if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = q + 1; }
+            }
+        }
+        if (best_axis >= 0) {
+            const int k = best_axis;
+            const float scale = kBins / (chi[k] - clo[k]);
+            auto it = std::partition(items.begin() + b, items.begin() + e, [&](uint32_t id) {
+                int q = static_cast<int>((tb[id].c[k] - clo[k]) * scale);
+                q = std::min(kBins - 1, std::max(0, q));
+                return q < best_split;
+            });
+            mid = static_cast<size_t>(it - items.begin());
+            if (mid == b || mid == e) mid = b + n / 2;
+        }
+        return mid;
+    }
+
+    void child_box(size_t b, size_t e, float* box) const
+    {
+        float lo[3], hi[3];
+        bounds(b, e, lo, hi);
+        for (int k = 0; k < 3; ++k) { box[k] = lo[k] - margin; box[3 + k] = hi[k] + margin; }
+    }
+
+    // Returns the child reference of the subtree over items[b, e); nodes in preorder, leaf
+    // slots in left-first DFS order.
     uint32_t build(size_t b, size_t e, int depth)
     {
         max_depth = std::max(max_depth, depth);
-        const size_t n = e - b;
-        if (n == 1) {
+        if (e - b == 1) {
             const uint32_t slot = static_cast<uint32_t>(out.leaf_order.size());
             out.leaf_order.push_back(items[b]);
             return PT_BVH_LEAF_FLAG | slot;
         }
-        size_t mid = b + n / 2;
-        if (n > 2) {
-            float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (size_t i = b; i < e; ++i)
-                for (int k = 0; k < 3; ++k) {
-                    clo[k] = std::min(clo[k], tb[items[i]].c[k]);
-                    chi[k] = std::max(chi[k], tb[items[i]].c[k]);
-                }
-            constexpr int kBins = 32;
-            float best_cost = INFINITY;
-            int best_axis = -1, best_split = 0;
-            for (int k = 0; k < 3; ++k) {
-                const float ext = chi[k] - clo[k];
-                if (!(ext > 0.0f)) continue;
-                int cnt[kBins] = {0};
-                float blo[kBins][3], bhi[kBins][3];
-                for (int q = 0; q < kBins; ++q)
-                    for (int j = 0; j < 3; ++j) { blo[q][j] = INFINITY; bhi[q][j] = -INFINITY; }
-                const float scale = kBins / ext;
-                for (size_t i = b; i < e; ++i) {
-                    const TriBox& t = tb[items[i]];
-                    int q = static_cast<int>((t.c[k] - clo[k]) * scale);
-                    q = std::min(kBins - 1, std::max(0, q));
-                    ++cnt[q];
-                    for (int j = 0; j < 3; ++j) { blo[q][j] = std::min(blo[q][j], t.lo[j]); bhi[q][j] = std::max(bhi[q][j], t.hi[j]); }
-                }
-                float rlo[kBins][3], rhi[kBins][3];
-                int rc[kBins];
-                float alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                int ac = 0;
-                for (int q = kBins - 1; q >= 0; --q) {
-                    for (int j = 0; j < 3; ++j) { alo[j] = std::min(alo[j], blo[q][j]); ahi[j] = std::max(ahi[j], bhi[q][j]); }
-                    ac += cnt[q];
-                    memcpy(rlo[q], alo, sizeof(alo));
-                    memcpy(rhi[q], ahi, sizeof(ahi));
-                    rc[q] = ac;
-                }
-                float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                int lc = 0;
-                for (int q = 0; q < kBins - 1; ++q) {
-                    for (int j = 0; j < 3; ++j) { llo[j] = std::min(llo[j], blo[q][j]); lhi[j] = std::max(lhi[j], bhi[q][j]); }
-                    lc += cnt[q];
-                    if (lc == 0 || rc[q + 1] == 0) continue;
-                    const float cost = lc * surface(llo, lhi) + rc[q + 1] * surface(rlo[q + 1], rhi[q + 1]);
-                    if (cost < best_cost) { best_cost = cost; best_axis = k; best_split = q + 1; }
-                }
-            }
-            if (best_axis >= 0) {
-                const int k = best_axis;
-                const float scale = kBins / (chi[k] - clo[k]);
-                auto it = std::partition(items.begin() + b, items.begin() + e, [&](uint32_t id) {
-                    int q = static_cast<int>((tb[id].c[k] - clo[k]) * scale);
-                    q = std::min(kBins - 1, std::max(0, q));
-                    return q < best_split;
-                });
-                mid = static_cast<size_t>(it - items.begin());
-                if (mid == b || mid == e) mid = b + n / 2;
-            }
-        }
+        const size_t mid = split(b, e);
         const uint32_t me = static_cast<uint32_t>(out.nodes.size());
         out.nodes.emplace_back();
         float box[2][6];
         const size_t ranges[2][2] = {{b, mid}, {mid, e}};
         uint32_t refs[2];
         for (int c = 0; c < 2; ++c) {
-            float lo[3], hi[3];
-            bounds(ranges[c][0], ranges[c][1], lo, hi);
-            for (int k = 0; k < 3; ++k) { box[c][k] = lo[k] - margin; box[c][3 + k] = hi[k] + margin; }
+            child_box(ranges[c][0], ranges[c][1], box[c]);
             refs[c] = build(ranges[c][0], ranges[c][1], depth + 1);
         }
         AccelNode& nd = out.nodes[me];
         memcpy(nd.box, box, sizeof(box));
         nd.child[0] = refs[0];
         nd.child[1] = refs[1];
+        return me;
+    }
+};
+
+// Parallel form of Builder::build with the identical result: the top levels are split serially
+// into ~4 subtrees per host thread, the subtrees are built concurrently into private arrays
+// (they only touch their own items range), then spliced in preorder with their node and leaf
+// indices offset -- exactly where the serial recursion would have emitted them.
+struct ParallelBuild {
+    struct Skel {
+        size_t b, e;
+        int depth;
+        int left = -1, right = -1;   // -1: a job
+        float box[2][6];
+        AccelBvh local;
+        uint32_t local_root = 0;
+        int local_depth = 0;
+    };
+    const std::vector<TriBox>& tb;
+    std::vector<uint32_t>& items;
+    float margin;
+    std::vector<Skel> skel;
+    std::vector<int> jobs;
+
+    int plan(Builder& planner, size_t b, size_t e, int depth, size_t cutoff)
+    {
+        const int me = static_cast<int>(skel.size());
+        skel.emplace_back();
+        skel[me].b = b; skel[me].e = e; skel[me].depth = depth;
+        if (e - b <= cutoff) { jobs.push_back(me); return me; }
+        const size_t mid = planner.split(b, e);
+        planner.child_box(b, mid, skel[me].box[0]);
+        planner.child_box(mid, e, skel[me].box[1]);
+        const int l = plan(planner, b, mid, depth + 1, cutoff);
+        const int r = plan(planner, mid, e, depth + 1, cutoff);
+        skel[me].left = l;
+        skel[me].right = r;
+        return me;
+    }
+
+    uint32_t emit(int k, AccelBvh& out, int* max_depth)
+    {
+        Skel& s = skel[k];
+        if (s.left < 0) {
+            const uint32_t no = static_cast<uint32_t>(out.nodes.size());
+            const uint32_t lo = static_cast<uint32_t>(out.leaf_order.size());
+            auto remap = [&](uint32_t ref) {
+                return (ref & PT_BVH_LEAF_FLAG) ? (PT_BVH_LEAF_FLAG | ((ref ^ PT_BVH_LEAF_FLAG) + lo)) : ref + no;
+            };
+            for (AccelNode nd : s.local.nodes) {
+                nd.child[0] = remap(nd.child[0]);
+                nd.child[1] = remap(nd.child[1]);
+                out.nodes.push_back(nd);
+            }
+            out.leaf_order.insert(out.leaf_order.end(), s.local.leaf_order.begin(), s.local.leaf_order.end());
+            *max_depth = std::max(*max_depth, s.local_depth);
+            return remap(s.local_root);
+        }
+        *max_depth = std::max(*max_depth, s.depth);
+        const uint32_t me = static_cast<uint32_t>(out.nodes.size());
+        out.nodes.emplace_back();
+        const uint32_t l = emit(s.left, out, max_depth);
+        const uint32_t r = emit(s.right, out, max_depth);
+        AccelNode& nd = out.nodes[me];
+        memcpy(nd.box, s.box, sizeof(s.box));
+        nd.child[0] = l;
+        nd.child[1] = r;
         return me;
     }
 };
@@ -165,13 +246,34 @@ int build_accel(const pt_scene& sc, AccelBvh* out)
     out->leaf_order.clear();
     out->nodes.reserve(nt);
     out->leaf_order.reserve(nt);
-    Builder bld(tb, items, *out, margin);
-    const uint32_t root = bld.build(0, nt, 0);
+    AccelBvh scratch;
+    Builder planner(tb, items, scratch, margin);
+    const unsigned threads = host_threads();
+    ParallelBuild pb{tb, items, margin, {}, {}};
+    pb.skel.reserve(64 * threads + 16);
+    const int top = pb.plan(planner, 0, nt, 0, std::max<size_t>(2048, nt / (4 * std::max(1u, threads))));
+    std::atomic<size_t> next_job{0};
+    auto worker = [&]() {
+        for (size_t j; (j = next_job.fetch_add(1)) < pb.jobs.size();) {
+            ParallelBuild::Skel& k = pb.skel[pb.jobs[j]];
+            Builder sub(tb, items, k.local, margin);
+            k.local.nodes.reserve(k.e - k.b);
+            k.local.leaf_order.reserve(k.e - k.b);
+            k.local_root = sub.build(k.b, k.e, k.depth);
+            k.local_depth = sub.max_depth;
+        }
+    };
+    std::vector<std::thread> ths;
+    for (unsigned t = 1; t < threads && t < pb.jobs.size(); ++t) ths.emplace_back(worker);
+    worker();
+    for (std::thread& t : ths) t.join();
+    int max_depth = 0;
+    const uint32_t root = pb.emit(top, *out, &max_depth);
     if (root != 0) return fail(PT_E_SCENE, "build_accel: internal error (root %u)", root);
     float lo[3], hi[3];
-    bld.bounds(0, nt, lo, hi);
+    planner.bounds(0, nt, lo, hi);
     for (int k = 0; k < 3; ++k) { out->root_box[k] = lo[k] - margin; out->root_box[3 + k] = hi[k] + margin; }
-    out->depth = bld.max_depth;
+    out->depth = max_depth;
     out->margin = margin;
     return PT_OK;
 }
@@ -252,3 +354,28 @@ int collapse_accel4(const AccelBvh& bin, Accel4* out)
 }
 
 }  // namespace pt
+
+// Host-side diagnostic (tests/test_host_surface.py): FNV-1a digest of the render-path BVH that
+// pt_create builds (binary SAH nodes + leaf order + BVH4 nodes), its BVH4 node count and depth.
+extern "C" int pt_accel_digest(const pt_scene* sc, uint64_t* digest, uint32_t* num_nodes4, int32_t* depth4)
+{
+    pt::clear_error();
+    if (!sc || !digest) return pt::fail(PT_E_INVALID, "pt_accel_digest: null argument");
+    pt::AccelBvh acc;
+    pt::Accel4 acc4;
+    int rc = pt::build_accel(*sc, &acc);
+    if (rc == PT_OK) rc = pt::collapse_accel4(acc, &acc4);
+    if (rc != PT_OK) return rc;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        const unsigned char* c = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) { h ^= c[i]; h *= 1099511628211ull; }
+    };
+    mix(acc.nodes.data(), acc.nodes.size() * sizeof(pt::AccelNode));
+    mix(acc.leaf_order.data(), acc.leaf_order.size() * sizeof(uint32_t));
+    mix(acc4.nodes.data(), acc4.nodes.size() * sizeof(acc4.nodes[0]));
+    *digest = h;
+    if (num_nodes4) *num_nodes4 = static_cast<uint32_t>(acc4.nodes.size());
+    if (depth4) *depth4 = acc4.depth;
+    return PT_OK;
+}

@@ -61,6 +61,9 @@ struct HostScene {
 // Deterministic float sin/cos shared with the kernels (defined in hip/pt_render.hip).
 void sincos_det(float theta, float* s, float* c);
 bool tonemap_thresholds(float t[256]);
+// host threads for the parallel builders: PT_HOST_THREADS, else OMP_NUM_THREADS, else the
+// hardware concurrency, capped at 16
+unsigned host_threads();
 
 // ---- render-path acceleration structure (accel_build.cpp) --------------------------------
 struct AccelNode {

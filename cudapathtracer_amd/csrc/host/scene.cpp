@@ -3,7 +3,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <new>
+#include <thread>
 
 #include "host_internal.h"
 
@@ -263,6 +265,18 @@ extern "C" int pt_write_pfm(const char* path, const float* rgb, int w, int h)
 }
 
 namespace pt {
+unsigned host_threads()
+{
+    for (const char* var : {"PT_HOST_THREADS", "OMP_NUM_THREADS"}) {
+        if (const char* e = getenv(var)) {
+            const int v = atoi(e);
+            if (v > 0) return static_cast<unsigned>(v < 64 ? v : 64);
+        }
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return hw == 0 ? 1u : (hw < 16 ? hw : 16u);
+}
+
 // Tone-map thresholds for the GPU output step: t[k] (k = 1..255) = the smallest non-negative
 // float c with pt_tonemap_u8(c) >= k.  The map is monotone in c (c/(c+1), pow, *255 and the
 // truncation all are), so for finite c >= 0 the code is the number of thresholds <= c, exactly

@@ -168,6 +168,12 @@ typedef struct {
     uint64_t shade_cycles;     /* same for shading (+ refill) phases                              */
 } pt_stats;
 
+/* Host-only diagnostic: builds the render path's private acceleration structure for `scene`
+ * exactly as pt_create does (SAH BVH collapsed to BVH4) and returns an FNV-1a digest
+ * of it, its BVH4 node count and depth.  Used to check that the parallel host build is
+ * deterministic. */
+int pt_accel_digest(const pt_scene* scene, uint64_t* digest, uint32_t* num_nodes4, int32_t* depth4);
+
 /* Upload a scene to HIP device `device` (ordinal among visible devices). */
 pt_ctx* pt_create(const pt_scene* scene, int device, int* err);
 

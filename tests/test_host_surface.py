@@ -187,3 +187,20 @@ def test_tonemap_threshold_table_reproduces_host_function():
     got = np.searchsorted(t[1:], probe, side="right")
     ref = np.array([pt.tonemap_u8(float(c)) for c in probe])
     assert np.array_equal(got, ref)
+
+
+def test_parallel_host_builds_are_deterministic(tmp_path, monkeypatch):
+    """The reference BVH (BVH.h) and the render path's SAH/BVH4 structure are built on several
+    host threads; both must equal the single-thread build exactly (the BVH.h array is also
+    pinned by the reference hashes above)."""
+    from cudapathtracer_amd import scenes
+    p = scenes.write_sponza_standin(str(tmp_path))
+    out = {}
+    for threads in ("1", "3", "8"):
+        monkeypatch.setenv("PT_HOST_THREADS", threads)
+        s = pt.Scene()
+        s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+        s.build_bvh()
+        out[threads] = (hashlib.sha256(s.arrays()["bvh"].tobytes()).hexdigest(), s.accel_digest())
+    assert out["1"] == out["3"] == out["8"]
+    assert out["1"][1][1] > 0 and out["1"][1][2] > 0
