@@ -14,6 +14,9 @@
 //   * breadth-first flattening: child index = current index + queue length after the push
 //     (:331-382); leaves are (triangle | 0x80000000).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <cfloat>
 #include <cmath>
@@ -103,7 +106,9 @@ public:
     int build_parallel(size_t nt, unsigned threads)
     {
         const size_t cutoff = std::max<size_t>(4096, nt / (4 * std::max(1u, threads)));
+        const auto c0 = std::chrono::steady_clock::now();
         const int top = plan(0, nt, 0, cutoff);
+        const auto c1 = std::chrono::steady_clock::now();
         std::atomic<size_t> next_job{0};
         auto worker = [&]() {
             for (size_t j; (j = next_job.fetch_add(1)) < jobs_.size();) {
@@ -115,6 +120,11 @@ public:
         for (unsigned t = 1; t < threads && t < jobs_.size(); ++t) pool.emplace_back(worker);
         worker();
         for (std::thread& t : pool) t.join();
+        const auto c2 = std::chrono::steady_clock::now();
+        if (getenv("PT_TIMING"))
+            fprintf(stderr, "build_bvh: %u threads, %zu jobs: plan %.1f ms, jobs %.1f ms\n", threads, jobs_.size(),
+                    std::chrono::duration<double, std::milli>(c1 - c0).count(),
+                    std::chrono::duration<double, std::milli>(c2 - c1).count());
         return finish(top);
     }
 

@@ -23,6 +23,7 @@
 #include <map>
 #include <sstream>
 #include <tuple>
+#include <unordered_map>
 
 #include "host_internal.h"
 
@@ -36,29 +37,27 @@ inline bool blank(char c) { return c == ' ' || c == '\t'; }
 inline bool line_end(char c) { return c == '\r' || c == '\n' || c == '\0'; }
 inline bool digit(char c) { return c >= '0' && c <= '9'; }
 
-// Split a whole file into the logical lines tinyobj's getline loop would see.
-std::vector<std::string> split_lines(const std::string& text)
+// Visit the logical lines tinyobj's getline loop would see, in place: each line is
+// NUL-terminated inside `text` (an embedded NUL ends the line early, as getline's C string
+// does); a line longer than kMaxLine is cut there and is the last line read (failbit).
+template <typename F>
+void for_each_line(std::string& text, F&& visit)
 {
-    std::vector<std::string> lines;
     size_t pos = 0;
     const size_t n = text.size();
+    char* base = &text[0];
     while (pos < n) {
-        size_t nl = text.find('\n', pos);
-        size_t stop = (nl == std::string::npos) ? n : nl;
-        std::string line = text.substr(pos, stop - pos);
-        if (line.size() > kMaxLine) {           // getline sets failbit: this is the last line read
-            line.resize(kMaxLine);
-            size_t z = line.find('\0');
-            if (z != std::string::npos) line.resize(z);
-            lines.push_back(line);
-            break;
+        const char* nl = static_cast<const char*>(memchr(base + pos, '\n', n - pos));
+        const size_t stop = nl ? static_cast<size_t>(nl - base) : n;
+        if (stop - pos > kMaxLine) {
+            base[pos + kMaxLine] = '\0';
+            visit(base + pos);
+            return;
         }
-        size_t z = line.find('\0');
-        if (z != std::string::npos) line.resize(z);
-        lines.push_back(line);
-        pos = (nl == std::string::npos) ? n : nl + 1;
+        if (stop < n) base[stop] = '\0';
+        visit(base + pos);
+        pos = nl ? stop + 1 : n;
     }
-    return lines;
 }
 
 bool slurp(const std::string& path, std::string* out)
@@ -72,12 +71,12 @@ bool slurp(const std::string& path, std::string* out)
 }
 
 // Returns a pointer to the first non-blank char of a trimmed line, or nullptr to skip it.
-const char* line_start(std::string& line)
+const char* line_start(char* line)
 {
-    if (!line.empty() && line.back() == '\n') line.pop_back();
-    if (!line.empty() && line.back() == '\r') line.pop_back();
-    if (line.empty()) return nullptr;
-    const char* t = line.c_str();
+    size_t len = strlen(line);
+    if (len > 0 && line[len - 1] == '\r') line[--len] = '\0';
+    if (len == 0) return nullptr;
+    const char* t = line;
     t += strspn(t, " \t");
     if (*t == '\0' || *t == '#') return nullptr;
     return t;
@@ -149,14 +148,14 @@ bool read_mtl(const std::string& path, std::vector<ObjMaterial>& mats, std::map<
     };
     reset();
     if (opened) {
-        for (std::string& line : split_lines(text)) {
+        for_each_line(text, [&](char* line) {
             const char* t = line_start(line);
-            if (!t) continue;
+            if (!t) return;
             if (strncmp(t, "newmtl", 6) == 0 && blank(t[6])) {
                 if (!cur.name.empty()) commit();
                 reset();
                 cur.name = first_word(t + 7);
-                continue;
+                return;
             }
             if (t[0] == 'K' && (t[1] == 'd' || t[1] == 'e') && blank(t[2])) {
                 float* dst = (t[1] == 'd') ? cur.diffuse : cur.emission;
@@ -165,26 +164,34 @@ bool read_mtl(const std::string& path, std::vector<ObjMaterial>& mats, std::map<
                 float g = next_real(t);
                 float b = next_real(t);
                 dst[0] = r; dst[1] = g; dst[2] = b;
-                continue;
+                return;
             }
             // Ka/Ks/Kt/Ni/Ns/illum/d/Tr/map_*/unknown keys do not reach loadOBJ.
-        }
+        });
     }
     commit();   // tinyobj always flushes the last (possibly default, unnamed) material
     return opened;
 }
 
-struct ShapeBuilder {
-    std::vector<std::vector<VIdx>> faces;
+// exportFaceGroupToShape (.cc:361-411) with a fresh vertex cache per shape.
+struct VIdxHash {
+    size_t operator()(const std::tuple<int, int, int>& k) const
+    {
+        uint64_t h = static_cast<uint32_t>(std::get<0>(k));
+        h = h * 0x9E3779B97F4A7C15ull ^ static_cast<uint32_t>(std::get<1>(k));
+        h = h * 0x9E3779B97F4A7C15ull ^ static_cast<uint32_t>(std::get<2>(k));
+        return static_cast<size_t>(h ^ (h >> 29));
+    }
 };
 
-// exportFaceGroupToShape (.cc:361-411) with a fresh vertex cache per shape.
-bool emit_shape(const std::vector<std::vector<VIdx>>& faces, const std::vector<float>& v, int material,
-                const std::string& name, std::vector<ObjShape>& shapes, std::string* err)
+// Faces are stored flat: face f has the index words fv[fstart[f] .. fstart[f+1]).
+bool emit_shape(const std::vector<VIdx>& fv, const std::vector<uint32_t>& fstart, const std::vector<float>& v,
+                int material, const std::string& name, std::vector<ObjShape>& shapes, std::string* err)
 {
-    if (faces.empty()) return true;
+    if (fstart.size() < 2) return true;
     ObjShape sh;
-    std::map<std::tuple<int, int, int>, uint32_t> seen;
+    std::unordered_map<std::tuple<int, int, int>, uint32_t, VIdxHash> seen;
+    seen.reserve(fv.size());
     auto vertex = [&](const VIdx& k, uint32_t* out) -> bool {
         auto key = std::make_tuple(k.v, k.vn, k.vt);
         auto it = seen.find(key);
@@ -201,10 +208,12 @@ bool emit_shape(const std::vector<std::vector<VIdx>>& faces, const std::vector<f
         *out = id;
         return true;
     };
-    for (const auto& f : faces) {
-        for (size_t k = 2; k < f.size(); ++k) {
+    for (size_t f = 0; f + 1 < fstart.size(); ++f) {
+        const VIdx* w = fv.data() + fstart[f];
+        const size_t cnt = fstart[f + 1] - fstart[f];
+        for (size_t k = 2; k < cnt; ++k) {
             uint32_t a, b, c;
-            if (!vertex(f[0], &a) || !vertex(f[k - 1], &b) || !vertex(f[k], &c)) return false;
+            if (!vertex(w[0], &a) || !vertex(w[k - 1], &b) || !vertex(w[k], &c)) return false;
             sh.indices.push_back(a);
             sh.indices.push_back(b);
             sh.indices.push_back(c);
@@ -214,6 +223,23 @@ bool emit_shape(const std::vector<std::vector<VIdx>>& faces, const std::vector<f
     sh.name = name;
     shapes.push_back(std::move(sh));
     return true;
+}
+
+// pow(10, -k) and pow(5, e) exactly as tryParseDouble computes them (the same libm calls),
+// tabulated once.
+struct PowTables {
+    double neg10[401];
+    double pow5[801];   // e in [-400, 400]
+    PowTables()
+    {
+        for (int k = 0; k <= 400; ++k) neg10[k] = pow(10.0, -k);
+        for (int e = -400; e <= 400; ++e) pow5[e + 400] = pow(5.0, e);
+    }
+};
+const PowTables& pow_tables()
+{
+    static const PowTables t;
+    return t;
 }
 
 }  // namespace
@@ -246,7 +272,7 @@ bool parse_real(const char* s, const char* end, double* out)
             ++p;
             int k = 1;
             while ((inside = (p != end)) && digit(*p)) {
-                m += static_cast<int>(*p - '0') * pow(10.0, -k);
+                m += static_cast<int>(*p - '0') * (k <= 400 ? pow_tables().neg10[k] : pow(10.0, -k));
                 ++k;
                 ++p;
             }
@@ -274,7 +300,7 @@ bool parse_real(const char* s, const char* end, double* out)
             if (ne == 0) return false;
         }
     }
-    *out = (negative ? -1 : 1) * ldexp(m * pow(5.0, e), e);
+    *out = (negative ? -1 : 1) * ldexp(m * ((e >= -400 && e <= 400) ? pow_tables().pow5[e + 400] : pow(5.0, e)), e);
     return true;
 }
 
@@ -289,57 +315,62 @@ ObjResult read_obj(const std::string& path, const std::string& mtl_basepath)
     }
     std::vector<float> v;
     int nvn = 0, nvt = 0;
-    std::vector<std::vector<VIdx>> faces;
+    std::vector<VIdx> fv;
+    std::vector<uint32_t> fstart(1, 0u);
     std::map<std::string, int> by_name;
     int material = -1;
     std::string name;
     std::string err;
     auto flush = [&]() -> bool {
-        if (!emit_shape(faces, v, material, name, res.shapes, &err)) return false;
-        faces.clear();
+        if (!emit_shape(fv, fstart, v, material, name, res.shapes, &err)) return false;
+        fv.clear();
+        fstart.assign(1, 0u);
         return true;
     };
-    for (std::string& line : split_lines(text)) {
+    bool stop = false;
+    for_each_line(text, [&](char* line) {
+        if (stop) return;
         const char* t = line_start(line);
-        if (!t) continue;
+        if (!t) return;
         if (t[0] == 'v' && blank(t[1])) {
             t += 2;
             float x = next_real(t);
             float y = next_real(t);
             float z = next_real(t);
             v.push_back(x); v.push_back(y); v.push_back(z);
-            continue;
+            return;
         }
-        if (t[0] == 'v' && t[1] == 'n' && blank(t[2])) { ++nvn; continue; }
-        if (t[0] == 'v' && t[1] == 't' && blank(t[2])) { ++nvt; continue; }
+        if (t[0] == 'v' && t[1] == 'n' && blank(t[2])) { ++nvn; return; }
+        if (t[0] == 'v' && t[1] == 't' && blank(t[2])) { ++nvt; return; }
         if (t[0] == 'f' && blank(t[1])) {
             t += 2;
             t += strspn(t, " \t");
-            std::vector<VIdx> f;
             while (!line_end(*t)) {
-                f.push_back(next_vidx(t, static_cast<int>(v.size() / 3), nvn, nvt));
+                fv.push_back(next_vidx(t, static_cast<int>(v.size() / 3), nvn, nvt));
                 t += strspn(t, " \t\r");
             }
-            faces.push_back(std::move(f));
-            continue;
+            fstart.push_back(static_cast<uint32_t>(fv.size()));
+            return;
         }
         if (strncmp(t, "usemtl", 6) == 0 && blank(t[6])) {
             std::string mname = first_word(t + 7);
-            if (!flush()) { res.message = err; res.fatal = true; return res; }
+            if (!flush()) { res.message = err; res.fatal = true; stop = true; return; }
             auto it = by_name.find(mname);
             material = (it != by_name.end()) ? it->second : -1;
-            continue;
+            return;
         }
         if (strncmp(t, "mtllib", 6) == 0 && blank(t[6])) {
             std::string lib = mtl_basepath + first_word(t + 7);
             if (!read_mtl(lib, res.materials, by_name)) {
                 res.message = "WARN: Material file [ " + lib + " ] not found. Created a default material.";
-                return res;   // tinyobj returns here: nothing after the mtllib line is read
+                stop = true;   // tinyobj returns here: nothing after the mtllib line is read
+                fv.clear();
+                fstart.assign(1, 0u);
             }
-            continue;
+            return;
         }
         if (t[0] == 'g' && blank(t[1])) {
-            if (!flush()) { res.message = err; res.fatal = true; return res; }
+            if (!flush()) { res.message = err; res.fatal = true; stop = true; return; }
             std::vector<std::string> words;
             while (!line_end(*t)) {
                 t += strspn(t, " \t");
@@ -349,14 +380,15 @@ ObjResult read_obj(const std::string& path, const std::string& mtl_basepath)
                 t += strspn(t, " \t\r");
             }
             name = (words.size() > 1) ? words[1] : std::string();
-            continue;
+            return;
         }
         if (t[0] == 'o' && blank(t[1])) {
-            if (!flush()) { res.message = err; res.fatal = true; return res; }
+            if (!flush()) { res.message = err; res.fatal = true; stop = true; return; }
             name = first_word(t + 2);
-            continue;
+            return;
         }
-    }
+    });
+    if (stop) return res;   // fatal error, or tinyobj's early return at a missing mtllib
     if (!flush()) { res.message = err; res.fatal = true; }
     return res;
 }
