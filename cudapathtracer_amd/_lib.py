@@ -21,7 +21,8 @@ PT_FLAG_NO_DEAD_PATH_SKIP = 0x2
 PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
-ABI_VERSION = 3                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
+PT_LIGHT_SPHERE = 0x80000000     # lights[] entry of an emissive sphere
+ABI_VERSION = 4                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -46,11 +47,16 @@ class Camera(C.Structure):
                 ("pxl_width", C.c_int32), ("pxl_height", C.c_int32)]
 
 
+class Sphere(C.Structure):   # sphere.h:7-12 (pt_sphere)
+    _fields_ = [("pos", Vec3), ("rad", C.c_float), ("diffuse", C.c_double * 3), ("emission", C.c_double * 3)]
+
+
 class SceneView(C.Structure):
     _fields_ = [("num_verts", C.c_uint32), ("num_tris", C.c_uint32), ("num_mats", C.c_uint32),
                 ("num_lights", C.c_uint32), ("verts", C.POINTER(Vec3)), ("tris", C.POINTER(Triangle)),
                 ("mats", C.POINTER(Material)), ("lights", C.POINTER(C.c_uint32)), ("total_light_area", C.c_float),
-                ("bvh", C.POINTER(BvhNode)), ("bvh_size", C.c_uint32), ("bvh_depth", C.c_int32)]
+                ("bvh", C.POINTER(BvhNode)), ("bvh_size", C.c_uint32), ("bvh_depth", C.c_int32),
+                ("spheres", C.POINTER(Sphere)), ("num_spheres", C.c_uint32)]
 
 
 class Params(C.Structure):
@@ -82,6 +88,7 @@ SIGNATURES = {
     "pt_scene_load_obj": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, Vec3, C.c_float, C.c_int]),
     "pt_scene_last_warning": (C.c_char_p, [C.c_void_p]),
     "pt_scene_build_bvh": (C.c_int, [C.c_void_p]),
+    "pt_scene_add_sphere": (C.c_int, [C.c_void_p, C.POINTER(Sphere)]),
     "pt_scene_view": (C.c_int, [C.c_void_p, C.POINTER(SceneView)]),
     "pt_morton_pxl_to_i": (C.c_uint32, [C.c_uint32, C.c_uint32]),
     "pt_morton_i_to_pxl": (None, [C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),

@@ -26,6 +26,7 @@ TRI = np.dtype([("v0", "<i4"), ("v1", "<i4"), ("v2", "<i4"), ("nx", "<f4"), ("ny
                 ("mat", "<i4")])
 MAT = np.dtype([("albedo", "<f8", (3,)), ("emission", "<f8", (3,))])
 NODE = np.dtype([("lo", "<f4", (3,)), ("hi", "<f4", (3,)), ("left", "<u4"), ("right", "<u4")])
+SPHERE = np.dtype([("pos", "<f4", (3,)), ("rad", "<f4"), ("diffuse", "<f8", (3,)), ("emission", "<f8", (3,))])
 
 
 def _arr(ptr, n, dtype):
@@ -99,7 +100,19 @@ class Scene:
             total_light_area=np.float32(v.total_light_area),
             bvh=_arr(v.bvh, v.bvh_size, NODE),
             bvh_depth=int(v.bvh_depth),
+            spheres=_arr(v.spheres, v.num_spheres, SPHERE),
         )
+
+    def add_sphere(self, pos, rad, diffuse, emission=(0.0, 0.0, 0.0)):
+        """sphere.h primitive (this build's semantics); returns self."""
+        sp = L.Sphere()
+        sp.pos = L.Vec3(*[float(v) for v in pos])
+        sp.rad = float(rad)
+        for k in range(3):
+            sp.diffuse[k] = float(diffuse[k])
+            sp.emission[k] = float(emission[k])
+        L.check(L.lib().pt_scene_add_sphere(self._h, C.byref(sp)))
+        return self
 
 
 def make_camera(pos=(0.0, 1.0, 3.0), dist_from_film=1.0, focal_length=3.0, radius=0.0, width=512, height=512):

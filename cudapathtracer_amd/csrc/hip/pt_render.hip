@@ -66,7 +66,57 @@ struct Args {
     uint32_t* pmemo;                // chunks > 1: primary hit of pixel slot q: [2q] = tri + 2 (0 = not yet), [2q+1] = t
     double* lbuf;                   // chunks > 1: per-sample radiance, channel k of sample n of pixel slot q
                                     // at lbuf[(k * spp + n-1) * npix + q]
+    const float4* spheres;          // sphere primitives: center xyz, radius (hit ids num_tris + i)
+    uint32_t num_spheres;
+    uint32_t num_tris;
+    uint32_t sphere_mat_base;       // material of sphere i = mats[sphere_mat_base + i]
 };
+
+__device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
+{
+    const float4 q = *reinterpret_cast<const float4*>(s + tri);
+    return v3(q.x, q.y, q.z);
+}
+__device__ __forceinline__ int32_t ld_mat(const DShade* s, int32_t tri) { return s[tri].mat; }
+
+// ------------------------------------------------------------------ spheres
+// The reference has sphere.h but no sphere code; the semantics are this build's, shared with
+// the oracle (or_sphere_t): unit d, oc = o - c, b = oc.d, disc = b*b - (oc.oc - r*r), nearer
+// root -b - sqrt(disc) if > 0, else -b + sqrt(disc) if > 0.  Spheres are tested after every
+// triangle with strict <, so a tie keeps the triangle.
+__device__ __forceinline__ float sphere_t(V3 o, V3 d, float4 sp)
+{
+    const V3 oc = o - v3(sp.x, sp.y, sp.z);
+    const float b = dot(oc, d);
+    const float c = dot(oc, oc) - sp.w * sp.w;
+    const float disc = b * b - c;
+    if (!(disc >= 0.0f)) return kMaxFloat;
+    const float q = sqrtf(disc);
+    float t = -b - q;
+    if (t > 0.0f) return t;
+    t = -b + q;
+    if (t > 0.0f) return t;
+    return kMaxFloat;
+}
+// closest of (htri, ht) and the spheres
+__device__ __forceinline__ void apply_spheres(const Args& a, V3 o, V3 d, int32_t* htri, float* ht)
+{
+    for (uint32_t k = 0; k < a.num_spheres; ++k) {
+        const float t = sphere_t(o, d, a.spheres[k]);
+        if (0.0f < t && t < *ht) { *ht = t; *htri = (int32_t)(a.num_tris + k); }
+    }
+}
+// primitive id -> material index / normal at p (spheres: (p - c) / r)
+__device__ __forceinline__ int32_t prim_mat(const Args& a, int32_t id)
+{
+    return ((uint32_t)id < a.num_tris) ? ld_mat(a.shade, id) : (int32_t)(a.sphere_mat_base + ((uint32_t)id - a.num_tris));
+}
+__device__ __forceinline__ V3 prim_normal(const Args& a, int32_t id, V3 p)
+{
+    if ((uint32_t)id < a.num_tris) return ld_norm(a.shade, id);
+    const float4 sp = a.spheres[(uint32_t)id - a.num_tris];
+    return (p - v3(sp.x, sp.y, sp.z)) / sp.w;
+}
 
 // ------------------------------------------------------------------ per-lane tracer
 template <bool kRefWalk, bool kCount>
@@ -85,9 +135,15 @@ struct Tracer {
     __device__ Hit trace(V3 o, V3 d)
     {
         ++traced;
-        if (kRefWalk)
-            return trace_reference<kCount>(o, d, a->rnodes, a->tris_orig, stack, lane, cnt);
-        return trace_culled<kCount>(o, d, a->root, a->nodes, a->tris_leaf, stack, lane, a->cull_rel, a->cull_abs, cnt);
+        Hit h;
+        h.tri = -1;
+        h.t = kMaxFloat;
+        if (a->num_tris > 0) {
+            if (kRefWalk) h = trace_reference<kCount>(o, d, a->rnodes, a->tris_orig, stack, lane, cnt);
+            else h = trace_culled<kCount>(o, d, a->root, a->nodes, a->tris_leaf, stack, lane, a->cull_rel, a->cull_abs, cnt);
+        }
+        if (a->num_spheres) apply_spheres(*a, o, d, &h.tri, &h.t);
+        return h;
     }
 
     __device__ Hit trace_primary(V3 o, V3 d, bool memo)
@@ -114,12 +170,6 @@ struct Tracer {
     }
 };
 
-__device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
-{
-    const float4 q = *reinterpret_cast<const float4*>(s + tri);
-    return v3(q.x, q.y, q.z);
-}
-__device__ __forceinline__ int32_t ld_mat(const DShade* s, int32_t tri) { return s[tri].mat; }
 
 // kernel.cu:44-54
 __device__ __forceinline__ V3 get_tangent(V3 n)
@@ -176,6 +226,15 @@ __device__ __forceinline__ int32_t pick_light(const Args& a, Rng& rng, V3* p)
     float u = rng_uniform(rng);
     float v = rng_uniform(rng);
     const DLight& L = a.lights[sel];
+    if (L.pad != 0.0f) {   // sphere light (d8): uniform point, z = 1 - 2u, phi = 2*3.14159*v
+        const float z = 1.0f - 2.0f * u;
+        const float rxy = sqrtf(__builtin_fmaxf(0.0f, 1.0f - z * z));
+        const float phi = (float)(2 * 3.14159 * (double)v);
+        float si, co;
+        det_sincos(phi, &si, &co);
+        *p = v3(L.v0[0], L.v0[1], L.v0[2]) + v3(rxy * co, rxy * si, z) * L.a1[0];
+        return L.tri;
+    }
     const V3 v0 = v3(L.v0[0], L.v0[1], L.v0[2]);
     const V3 a1 = v3(L.a1[0], L.a1[1], L.a1[2]);
     const V3 a2 = v3(L.a2[0], L.a2[1], L.a2[2]);
@@ -212,10 +271,9 @@ __device__ C3 radiance_unidir(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 o,
         float t = (float)((double)h.t - 0.001);                                 // :431
         if ((double)t < 0.001) weight = c3(0, 0, 0);                             // :432
         if (t > kMaxFloat - 1) { weight = c3(0, 0, 0); tri = 0; t = 0; }         // :436
-        const int32_t mi = ld_mat(a.shade, tri);
-        const DMat* cm = a.mats + mi;
-        const V3 normal = ld_norm(a.shade, tri);
         const V3 pos = o + dir * t;                                               // :449
+        const DMat* cm = a.mats + prim_mat(a, tri);
+        const V3 normal = prim_normal(a, tri, pos);
         if (cm->emission[0] != 0) {                                               // :453
             accum = cadd(accum, cmul(weight, mat_emission(cm)));
             weight = c3(0, 0, 0);
@@ -264,10 +322,10 @@ __device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_
     {
         V3 p;
         const int32_t sel = pick_light(a, rng, &p);
-        const V3 n = ld_norm(a.shade, sel);
+        const V3 n = prim_normal(a, sel, p);
         x[0] = p + n * 0.001f;
         nrm[0] = n;
-        mat[0] = ld_mat(a.shade, sel);
+        mat[0] = prim_mat(a, sel);
         ip[0] = a.total_light_area;
     }
     {
@@ -276,10 +334,10 @@ __device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_
         int32_t tri = h.tri;
         float t = (float)((double)h.t - 0.001);
         if (t > kMaxFloat - 1) { tri = 0; t = 0; }
-        const V3 n2 = ld_norm(a.shade, tri);
         const V3 pos = x[0] + od * t;
+        const V3 n2 = prim_normal(a, tri, pos);
         const float G = __builtin_fabsf(dot(n2, od)) / __builtin_fmaxf(0.001f, t * t);
-        x[1] = pos; nrm[1] = n2; mat[1] = ld_mat(a.shade, tri);
+        x[1] = pos; nrm[1] = n2; mat[1] = prim_mat(a, tri);
         ip[1] = (float)(2 * 3.14159 / (double)G);
     }
     x[4] = cam_o; nrm[4] = cam_d; ip[4] = 1;
@@ -289,8 +347,8 @@ __device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_
         float t = (float)((double)h.t - 0.001);
         if (t > kMaxFloat - 1) { tri = 0; t = 0; }
         x[3] = cam_o + cam_d * t;
-        nrm[3] = ld_norm(a.shade, tri);
-        mat[3] = ld_mat(a.shade, tri);
+        nrm[3] = prim_normal(a, tri, x[3]);
+        mat[3] = prim_mat(a, tri);
         ip[3] = 1;
     }
     {
@@ -299,13 +357,13 @@ __device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_
         int32_t tri = h.tri;
         float t = (float)((double)h.t - 0.001);
         if (t > kMaxFloat - 1 || tri < 0) { tri = 0; t = 0; }
-        const V3 n = ld_norm(a.shade, tri);
+        x[2] = x[3] + d * t;
+        const V3 n = prim_normal(a, tri, x[2]);
         float G = __builtin_fabsf(dot(nrm[3], d) * dot(n, d)) / (t * t);
         if (G == 0) G = 1;
         if (G != G) G = 1;
-        x[2] = x[3] + d * t;
         nrm[2] = n;
-        mat[2] = ld_mat(a.shade, tri);
+        mat[2] = prim_mat(a, tri);
         ip[2] = (float)(3.14159 / (double)G);
     }
     C3 accum = c3(0, 0, 0);
@@ -474,7 +532,8 @@ enum : int {
 };
 // CF_OWNER: chunk 0 of a split pixel (publishes its primary hit in pmemo); CF_SHARE: a later
 // chunk (takes the published hit instead of tracing the camera ray again)
-enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16 };
+// CF_MEMO: the pending hit came from the memo (already includes spheres)
+enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32 };
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the word
 // offset k * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -677,6 +736,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             // a ray outside the Markstein preconditions, which takes the exact slow walk)
             auto begin_trace = [&](V3 o, V3 d) -> bool {
                 wave_count(lcnt + 0, lane);
+                if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }   // spheres only
                 if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
                 if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
                     htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
@@ -696,7 +756,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 wave_count(lcnt + 1, lane);
                 if (fl & CF_HAVE) {
                     htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
-                    fl &= ~CF_PRIMARY; state = ST_SHADE;
+                    fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
                     return true;
                 }
                 if (fl & CF_SHARE) {
@@ -706,7 +766,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     if (tv != 0u) {
                         htri = (int32_t)(tv - 2u);
                         ht = __uint_as_float(a.pmemo[2 * (size_t)q + 1]);
-                        fl = (fl | CF_PRIMARY) & ~CF_SHARE;   // stores the unit memo on shading
+                        fl = (fl | CF_PRIMARY | CF_MEMO) & ~CF_SHARE;   // stores the unit memo on shading
                         state = ST_SHADE;
                         return true;
                     }
@@ -724,6 +784,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                                &htri, &ht);
                 }
                 state = ST_SHADE;
+                if (a.num_spheres && !(fl & CF_MEMO)) apply_spheres(a, ro, rd, &htri, &ht);
+                fl &= ~CF_MEMO;
                 if (fl & CF_PRIMARY) {
                     fl = (fl | CF_HAVE) & ~CF_PRIMARY;
                     R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
@@ -741,10 +803,9 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     float t = (float)((double)ht - 0.001);
                     if ((double)t < 0.001) wgt = c3(0, 0, 0);
                     if (t > kMaxFloat - 1) { wgt = c3(0, 0, 0); tri = 0; t = 0; }
-                    const int32_t mi = ld_mat(a.shade, tri);
-                    const DMat* cm = a.mats + mi;
-                    const V3 normal = ld_norm(a.shade, tri);
                     const V3 pos = ro + rd * t;
+                    const DMat* cm = a.mats + prim_mat(a, tri);
+                    const V3 normal = prim_normal(a, tri, pos);
                     if (cm->emission[0] != 0) {
                         C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
                         acc = cadd(acc, cmul(wgt, mat_emission(cm)));
@@ -936,7 +997,9 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
         const V3 d = v3(rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]);
         int32_t htri = -1;
         float ht = kMaxFloat;
-        if (kRef) {
+        if (a.num_tris == 0) {
+            // spheres only
+        } else if (kRef) {
             const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
             htri = h.tri; ht = h.t;
         } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
@@ -960,6 +1023,7 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
                 }
             }
         }
+        if (a.num_spheres) apply_spheres(a, o, d, &htri, &ht);
         tri_out[r] = htri;
         t_out[r] = ht;
     }
@@ -1077,6 +1141,9 @@ struct pt_ctx {
     size_t pmemo_words = 0;
     float* tone_thr = nullptr;        // output step: the host libm's 255 code boundaries (+ t[0] = 0)
     bool tone_ok = false;
+    float4* spheres = nullptr;        // sphere primitives (center, radius)
+    uint32_t num_spheres = 0;
+    uint32_t sphere_mat_base = 0;
     float acc_root[6];
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
@@ -1101,10 +1168,14 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         tstart = now;
     };
     auto bail = [&](int code) -> pt_ctx* { if (err) *err = code; return nullptr; };
-    if (!sc || !sc->verts || !sc->tris || !sc->mats || !sc->bvh) return bail(pt::fail(PT_E_INVALID, "pt_create: incomplete scene"));
-    if (sc->num_tris < 2 || sc->bvh_size != sc->num_tris - 1)
-        return bail(pt::fail(PT_E_SCENE, "pt_create: need >= 2 triangles and a BVH of num_tris-1 nodes (got %u tris, %u nodes)",
-                             sc->num_tris, sc->bvh_size));
+    if (!sc || (sc->num_tris == 0 && sc->num_spheres == 0) || (sc->num_tris > 0 && (!sc->verts || !sc->tris || !sc->bvh)) ||
+        (sc->num_mats > 0 && !sc->mats) ||
+        (sc->num_spheres > 0 && !sc->spheres) || (sc->num_lights > 0 && !sc->lights))
+        return bail(pt::fail(PT_E_INVALID, "pt_create: incomplete scene"));
+    const bool spheres_only = sc->num_tris == 0 && sc->num_spheres > 0 && sc->bvh_size == 0;
+    if (!spheres_only && (sc->num_tris < 2 || sc->bvh_size != sc->num_tris - 1))
+        return bail(pt::fail(PT_E_SCENE, "pt_create: need >= 2 triangles and a BVH of num_tris-1 nodes, or spheres only "
+                             "(got %u tris, %u nodes, %u spheres)", sc->num_tris, sc->bvh_size, sc->num_spheres));
     if (sc->bvh_depth >= PT_MAX_BVH_DEPTH)
         return bail(pt::fail(PT_E_BVH_DEPTH, "Critical Error: BVH depth is too big (%d)", sc->bvh_depth));
     int ndev = 0;
@@ -1123,14 +1194,20 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             (uint32_t)t.mat >= sc->num_mats)
             return bail(pt::fail(PT_E_SCENE, "pt_create: triangle %u has an out-of-range vertex or material index", i));
     }
-    for (uint32_t j = 0; j < sc->num_lights; ++j)
-        if (sc->lights[j] >= nt) return bail(pt::fail(PT_E_SCENE, "pt_create: light %u indexes triangle %u", j, sc->lights[j]));
+    for (uint32_t j = 0; j < sc->num_lights; ++j) {
+        const uint32_t e = sc->lights[j];
+        if ((e & PT_LIGHT_SPHERE) ? (e ^ PT_LIGHT_SPHERE) >= sc->num_spheres : e >= nt)
+            return bail(pt::fail(PT_E_SCENE, "pt_create: light %u has an out-of-range primitive (0x%x)", j, e));
+    }
+    for (uint32_t k = 0; k < sc->num_spheres; ++k)
+        if (!(sc->spheres[k].rad > 0.0f) || !std::isfinite(sc->spheres[k].rad))
+            return bail(pt::fail(PT_E_SCENE, "pt_create: sphere %u has radius %g", k, (double)sc->spheres[k].rad));
     // validate the BVH: every reference must be in range, every triangle reachable once
     lap("device query");
     std::vector<uint32_t> leaf_rank(nt, 0xffffffffu);
     std::vector<uint32_t> leaf_order;
     leaf_order.reserve(nt);
-    {
+    if (nt > 0) {
         std::vector<uint32_t> st;
         st.push_back(0);
         size_t visits = 0;
@@ -1205,11 +1282,19 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         dn[i].c = make_float4(b1[2], b1[3], b1[4], b1[5]);
         dn[i].d = make_uint4(remap(x.left), remap(x.right), 0u, 0u);
     }
-    {
+    if (nt > 0) {
         const pt_bvh_node& r = sc->bvh[0];
         c->root[0] = r.lo.x; c->root[1] = r.lo.y; c->root[2] = r.lo.z;
         c->root[3] = r.hi.x; c->root[4] = r.hi.y; c->root[5] = r.hi.z;
         for (int q = 0; q < 3; ++q) { lo_all[q] = c->root[q]; hi_all[q] = c->root[3 + q]; }
+    }
+    for (uint32_t k = 0; k < sc->num_spheres; ++k) {   // the scene extent covers the spheres too
+        const pt_sphere& sp = sc->spheres[k];
+        const float cc[3] = {sp.pos.x, sp.pos.y, sp.pos.z};
+        for (int q = 0; q < 3; ++q) {
+            lo_all[q] = std::fmin(lo_all[q], cc[q] - sp.rad);
+            hi_all[q] = std::fmax(hi_all[q], cc[q] + sp.rad);
+        }
     }
     {
         float ext = 0.0f;
@@ -1246,7 +1331,11 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
     std::vector<DNode4> an;
     std::vector<DTri> at;
-    {
+    if (nt == 0) {   // spheres only: no triangle structures (kernels skip the walk)
+        for (int q = 0; q < 3; ++q) { c->acc_root[q] = INFINITY; c->acc_root[3 + q] = -INFINITY; }
+        c->acc4_depth = 0;
+        c->node4_mask = 1u;
+    } else {
         pt::AccelBvh acc;
         pt::Accel4 acc4;
         lap("reference-BVH records");
@@ -1285,10 +1374,20 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
         sh[i].mat = sc->tris[i].mat;
     }
-    std::vector<DMat> mt(sc->num_mats);
+    // scene materials, then one per sphere (sphere.h diffuse / emm)
+    std::vector<DMat> mt(sc->num_mats + sc->num_spheres);
     for (uint32_t i = 0; i < sc->num_mats; ++i) {
         for (int q = 0; q < 3; ++q) { mt[i].albedo[q] = sc->mats[i].albedo[q]; mt[i].emission[q] = sc->mats[i].emission[q]; }
     }
+    for (uint32_t k = 0; k < sc->num_spheres; ++k) {
+        DMat& m = mt[sc->num_mats + k];
+        for (int q = 0; q < 3; ++q) { m.albedo[q] = sc->spheres[k].diffuse[q]; m.emission[q] = sc->spheres[k].emission[q]; }
+    }
+    std::vector<float4> sp(sc->num_spheres);
+    for (uint32_t k = 0; k < sc->num_spheres; ++k)
+        sp[k] = make_float4(sc->spheres[k].pos.x, sc->spheres[k].pos.y, sc->spheres[k].pos.z, sc->spheres[k].rad);
+    c->num_spheres = sc->num_spheres;
+    c->sphere_mat_base = sc->num_mats;
     std::vector<DLight> lt(sc->num_lights + 1);
     auto light_rec = [&](uint32_t tri) {
         const pt_triangle& t = sc->tris[tri];
@@ -1306,8 +1405,23 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         L.pad = 0.0f;
         return L;
     };
-    for (uint32_t j = 0; j < sc->num_lights; ++j) lt[j] = light_rec(sc->lights[j]);
-    lt[sc->num_lights] = light_rec(0);
+    // sphere light (d8 policy): area 4*3.14159*r^2, center in v0, radius in a1[0], pad = 1
+    auto sphere_light = [&](uint32_t k) {
+        DLight L;
+        memset(&L, 0, sizeof(L));
+        const pt_sphere& q = sc->spheres[k];
+        L.area = pt::sphere_area(q.rad);
+        L.tri = (int32_t)(nt + k);
+        L.v0[0] = q.pos.x; L.v0[1] = q.pos.y; L.v0[2] = q.pos.z;
+        L.a1[0] = q.rad;
+        L.pad = 1.0f;
+        return L;
+    };
+    for (uint32_t j = 0; j < sc->num_lights; ++j) {
+        const uint32_t e = sc->lights[j];
+        lt[j] = (e & PT_LIGHT_SPHERE) ? sphere_light(e ^ PT_LIGHT_SPHERE) : light_rec(e);
+    }
+    lt[sc->num_lights] = (nt > 0) ? light_rec(0) : sphere_light(0);   // "nothing picked": primitive 0
     c->num_lights = sc->num_lights;
     c->total_light_area = sc->total_light_area;
     std::vector<uint32_t> jump_img, jump;
@@ -1320,7 +1434,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     lap("records + jump/tone tables");
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
-        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) ||
+        (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
         (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar))) {
         pt_destroy(c);
         return bail(rc);
@@ -1344,7 +1458,7 @@ void pt_destroy(pt_ctx* c)
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
-                    c->tone_thr};
+                    c->tone_thr, c->spheres};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1374,6 +1488,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.shade = c->shade; a.mats = c->mats; a.lights = c->lights; a.jump = c->jump;
     a.out = d_out; a.counters = c->counters; a.tile_counter = c->tile_counter;
     a.num_lights = c->num_lights; a.total_light_area = c->total_light_area;
+    a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;
+    a.sphere_mat_base = c->sphere_mat_base;
     memcpy(a.root, c->root, sizeof(a.root));
     a.cam.pos[0] = cam->pos.x; a.cam.pos[1] = cam->pos.y; a.cam.pos[2] = cam->pos.z;
     a.cam.dist = cam->dist_from_film; a.cam.focal = cam->focal_length; a.cam.radius = cam->radius;
@@ -1570,6 +1686,8 @@ extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_o
     memset(&a, 0, sizeof(a));
     a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
     a.counters = c->counters;
+    a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;
+    a.sphere_mat_base = c->sphere_mat_base;
     memcpy(a.root, c->root, sizeof(a.root));
     memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
     a.cull_rel = 1.0f + 1.0f / 1024.0f;

@@ -11,6 +11,7 @@
 static_assert(sizeof(pt_vec3) == 12, "vec3 is 12 B (vec3.h:4-7)");
 static_assert(sizeof(pt_triangle) == 28, "triangle is 28 B (modelLoader.h:14-19)");
 static_assert(sizeof(pt_material) == 48, "materialDesc is 48 B (modelLoader.h:21-25)");
+static_assert(sizeof(pt_sphere) == 64, "sphere.h sphere is 64 B");
 static_assert(sizeof(pt_bvh_node) == 32, "BVH_array_node is 32 B (BVH.h:111-115)");
 static_assert(sizeof(pt_camera) == 32, "camera is 32 B (camera.h:26-34)");
 
@@ -55,8 +56,12 @@ struct HostScene {
     float total_light_area = 0.0f;
     std::vector<pt_bvh_node> bvh;
     int32_t bvh_depth = 0;
+    std::vector<pt_sphere> spheres;
     std::string warning;
 };
+
+// Area of an emissive sphere light: 4*3.14159*r^2 evaluated in float, left to right.
+inline float sphere_area(float r) { return 4.0f * 3.14159f * r * r; }
 
 // Deterministic float sin/cos shared with the kernels (defined in hip/pt_render.hip).
 void sincos_det(float theta, float* s, float* c);

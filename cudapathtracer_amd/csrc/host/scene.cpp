@@ -122,10 +122,30 @@ int pt_scene_load_obj(pt_host_scene* hs, const char* obj_path, const char* mtl_b
     return PT_OK;
 }
 
+int pt_scene_add_sphere(pt_host_scene* hs, const pt_sphere* sp)
+{
+    if (!hs || !sp) return fail(PT_E_INVALID, "pt_scene_add_sphere: null argument");
+    if (!(sp->rad > 0.0f) || !std::isfinite(sp->rad) || !std::isfinite(sp->pos.x) || !std::isfinite(sp->pos.y) ||
+        !std::isfinite(sp->pos.z))
+        return fail(PT_E_INVALID, "pt_scene_add_sphere: radius must be > 0 and the sphere finite");
+    HostScene& s = hs->s;
+    if (sp->emission[0] != 0) {
+        s.lights.push_back(PT_LIGHT_SPHERE | static_cast<uint32_t>(s.spheres.size()));
+        s.total_light_area += sphere_area(sp->rad);
+    }
+    s.spheres.push_back(*sp);
+    return PT_OK;
+}
+
 int pt_scene_build_bvh(pt_host_scene* hs)
 {
     if (!hs) return fail(PT_E_INVALID, "pt_scene_build_bvh: null scene");
     HostScene& s = hs->s;
+    if (s.tris.empty() && !s.spheres.empty()) {   // spheres only: no triangle BVH (config C1)
+        s.bvh.clear();
+        s.bvh_depth = 0;
+        return PT_OK;
+    }
     int rc = build_bvh(s.verts, s.tris, &s.bvh, &s.bvh_depth);
     if (rc != PT_OK) return rc;
     if (s.bvh_depth >= PT_MAX_BVH_DEPTH)                                        // kernel.cu:627-631
@@ -149,6 +169,8 @@ int pt_scene_view(const pt_host_scene* hs, pt_scene* out)
     out->bvh = s.bvh.data();
     out->bvh_size = static_cast<uint32_t>(s.bvh.size());
     out->bvh_depth = s.bvh_depth;
+    out->spheres = s.spheres.data();
+    out->num_spheres = static_cast<uint32_t>(s.spheres.size());
     return PT_OK;
 }
 

@@ -438,3 +438,27 @@ def write_sponza_standin(dirpath, name="sponza_standin", scale_tris=STANDIN_SCAL
 
 def standin_triangle_count(scale_tris=STANDIN_SCALE):
     return int(sum(len(t) for _, _, t in sponza_standin_meshes(scale_tris)))
+
+
+# ----------------------------------------------------------------------------- spheres (C1)
+# A Cornell box made of sphere.h spheres only: walls are radius-100
+# spheres (f32-friendly: the quadratic's oc.oc - r^2 cancels ~1e4, not smallpt's 1e10), two
+# diffuse balls and a small emissive sphere under the ceiling.  Camera: CORNELL_CAMERA.
+CORNELL_SPHERES = [
+    # pos, rad, diffuse, emission
+    ((-101.0, 1.0, 0.0), 100.0, (0.75, 0.25, 0.25), (0.0, 0.0, 0.0)),     # left wall
+    ((101.0, 1.0, 0.0), 100.0, (0.25, 0.25, 0.75), (0.0, 0.0, 0.0)),      # right wall
+    ((0.0, 1.0, -101.0), 100.0, (0.75, 0.75, 0.75), (0.0, 0.0, 0.0)),     # back wall
+    ((0.0, -100.0, 0.0), 100.0, (0.75, 0.75, 0.75), (0.0, 0.0, 0.0)),     # floor
+    ((0.0, 102.0, 0.0), 100.0, (0.75, 0.75, 0.75), (0.0, 0.0, 0.0)),      # ceiling
+    ((-0.45, 0.35, -0.3), 0.35, (0.9, 0.9, 0.9), (0.0, 0.0, 0.0)),
+    ((0.45, 0.35, 0.3), 0.35, (0.9, 0.9, 0.9), (0.0, 0.0, 0.0)),
+    ((0.0, 1.85, 0.0), 0.12, (0.0, 0.0, 0.0), (12.0, 12.0, 12.0)),         # light
+]
+
+
+def add_cornell_spheres(scene, spheres=CORNELL_SPHERES):
+    """Append the C1 spheres to a pt.Scene (returns it)."""
+    for pos, rad, diffuse, emission in spheres:
+        scene.add_sphere(pos, rad, diffuse, emission)
+    return scene

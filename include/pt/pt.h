@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3
+#define PT_ABI_VERSION 4
 
 /* ---- status codes */
 #define PT_OK 0
@@ -60,6 +60,13 @@ typedef struct {                                                                
 
 #define PT_BVH_LEAF_FLAG 0x80000000u   /* limits.h:6 */
 #define PT_MAX_BVH_DEPTH 64            /* kernel.cu:35 */
+#define PT_LIGHT_SPHERE 0x80000000u    /* lights[] entry: PT_LIGHT_SPHERE | sphere index    */
+
+/* sphere.h:7-12 (64 B).  The reference has the struct but no intersection code (its include is
+ * commented out, kernel.cu:21); the semantics here are this build's:
+ * hit ids num_tris + i, closest root with 0 < t < MAX_FLOAT, normal (p - pos) / rad, material
+ * {diffuse, emission}; emissive spheres are area lights of area 4*3.14159*rad^2. */
+typedef struct { pt_vec3 pos; float rad; double diffuse[3]; double emission[3]; } pt_sphere;
 
 /* Read-only view of a scene: sceneDesc (modelLoader.h:29-41) + BVH_array (BVH.h:116-121). */
 typedef struct {
@@ -70,8 +77,10 @@ typedef struct {
     const uint32_t* lights;
     float total_light_area;
     const pt_bvh_node* bvh;    /* breadth-first array, node 0 = root            */
-    uint32_t bvh_size;         /* = num_tris - 1                                 */
+    uint32_t bvh_size;         /* = num_tris - 1 (0 for a scene of spheres only) */
     int32_t bvh_depth;         /* BVH_node::depth of the root (BVH.h:322, :346)  */
+    const pt_sphere* spheres;  /* sphere primitives (hit ids num_tris + i)      */
+    uint32_t num_spheres;
 } pt_scene;
 
 /* ======================================================================= host surface */
@@ -94,6 +103,10 @@ const char* pt_scene_last_warning(const pt_host_scene* s);
 /* buildBVH() -- BVH.h:443-474, byte-identical node array.  Fails with PT_E_SCENE for
  * fewer than 2 triangles (decision d5) and PT_E_BVH_DEPTH when depth >= 64. */
 int pt_scene_build_bvh(pt_host_scene* s);
+
+/* Append a sphere primitive (sphere.h); an emissive one (emission[0] != 0, the triangle rule of
+ * modelLoader.h:188) joins the light list and totalLightArea.  rad must be finite and > 0. */
+int pt_scene_add_sphere(pt_host_scene* scene, const pt_sphere* sphere);
 
 /* Borrow a view of the scene arrays (valid until the next mutation or pt_scene_free). */
 int pt_scene_view(const pt_host_scene* s, pt_scene* out);

@@ -37,11 +37,16 @@ class OXorwow(C.Structure):
     _fields_ = [("d", C.c_uint32), ("v", C.c_uint32 * 5)]
 
 
+class OSphere(C.Structure):
+    _fields_ = [("pos", OVec3), ("rad", C.c_float), ("diffuse", C.c_double * 3), ("emission", C.c_double * 3)]
+
+
 class OScene(C.Structure):
     _fields_ = [("num_verts", C.c_uint32), ("num_tris", C.c_uint32), ("num_mats", C.c_uint32),
                 ("num_lights", C.c_uint32), ("verts", C.c_void_p), ("tris", C.c_void_p), ("mats", C.c_void_p),
                 ("lights", C.c_void_p), ("total_light_area", C.c_float), ("bvh", C.c_void_p),
-                ("bvh_size", C.c_uint32)]
+                ("bvh_size", C.c_uint32),
+                ("spheres", C.c_void_p), ("num_spheres", C.c_uint32)]
 
 
 class OCounters(C.Structure):
@@ -100,8 +105,12 @@ class OracleScene:
         s.verts, s.tris, s.mats = self.verts.ctypes.data, self.tris.ctypes.data, self.mats.ctypes.data
         s.lights = self.lights.ctypes.data if len(self.lights) else None
         s.total_light_area = float(arrays["total_light_area"])
-        s.bvh = self.bvh.ctypes.data
+        s.bvh = self.bvh.ctypes.data if len(self.bvh) else None
         s.bvh_size = len(self.bvh)
+        sph = arrays.get("spheres")
+        self.spheres = np.ascontiguousarray(sph) if sph is not None and len(sph) else None
+        s.spheres = self.spheres.ctypes.data if self.spheres is not None else None
+        s.num_spheres = 0 if self.spheres is None else len(self.spheres)
         self.c = s
 
 

@@ -289,6 +289,44 @@ void or_camera_ray(const or_camera* cam, uint32_t idx, float u1, float u2, or_ve
     *d_out = vnormalized(vsub(film, o));
 }
 
+/* ------------------------------------------------------------- spheres (d8) */
+/* Ray/sphere for unit d, in float and in this order: oc = o - c, b = oc.d,
+ * disc = b*b - (oc.oc - r*r); the nearer root -b - sqrt(disc) if > 0, else -b + sqrt(disc)
+ * if > 0, else a miss (MAX_FLOAT).  The caller keeps it only if t < closestT (strict). */
+float or_sphere_t(or_vec3 o, or_vec3 d, const or_sphere* s)
+{
+    or_vec3 oc = vsub(o, s->pos);
+    float b = vdot(oc, d);
+    float c = vdot(oc, oc) - s->rad * s->rad;
+    float disc = b * b - c;
+    if (!(disc >= 0.0f)) return OR_MAX_FLOAT;
+    float q = sqrtf(disc);
+    float t = -b - q;
+    if (t > 0.0f) return t;
+    t = -b + q;
+    if (t > 0.0f) return t;
+    return OR_MAX_FLOAT;
+}
+
+static inline float sphere_area(float r) { return 4.0f * 3.14159f * r * r; }
+
+/* primitive id -> material handle / normal at p (triangles: modelLoader.h:14-19; spheres:
+ * material num_mats + i, normal (p - c) / r) */
+static inline int32_t prim_mat(const or_scene* sc, int32_t id)
+{
+    return (uint32_t)id < sc->num_tris ? sc->tris[id].mat : (int32_t)(sc->num_mats + ((uint32_t)id - sc->num_tris));
+}
+static inline const or_mat* mat_ptr(const or_scene* sc, int32_t m)
+{
+    return (uint32_t)m < sc->num_mats ? sc->mats + m : (const or_mat*)(const void*)sc->spheres[(uint32_t)m - sc->num_mats].diffuse;
+}
+static inline or_vec3 prim_normal(const or_scene* sc, int32_t id, or_vec3 p)
+{
+    if ((uint32_t)id < sc->num_tris) return sc->tris[id].norm;
+    const or_sphere* s = sc->spheres + ((uint32_t)id - sc->num_tris);
+    return vdiv(vsub(p, s->pos), s->rad);
+}
+
 /* ------------------------------------------------------------- traversal */
 /* kernel.cu:112-161 trace(): explicit stack, left child on top, strict 0<t<closestT. */
 int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float* t_out, or_counters* cnt)
@@ -299,6 +337,7 @@ int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float
     int32_t tri = -1;
     int i = 0;
     uint64_t nt = 0, tt = 0;
+    if (sc->bvh_size == 0) i = -1;             /* no triangles */
     while (i >= 0) {
         uint32_t e = stack[i];
         if (e & OR_LEAF_FLAG) {
@@ -319,6 +358,10 @@ int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float
                 --i;
             }
         }
+    }
+    for (uint32_t k = 0; k < sc->num_spheres; ++k) {       /* after every triangle: ties keep the triangle */
+        float t = or_sphere_t(o, dir, sc->spheres + k);
+        if (0.0f < t && t < closest) { closest = t; tri = (int32_t)(sc->num_tris + k); }
     }
     *tri_out = tri;
     *t_out = closest;
@@ -380,21 +423,42 @@ static or_vec3 cosine_ray(or_vec3 n, or_xorwow* rng)                   /* kernel
 static col brdf(const or_mat* m) { return cmulf(mat_albedo(m), (float)(1 / 3.14159)); }  /* kernel.cu:101-104 */
 
 /* Area-CDF light pick + uniform point (kernel.cu:466-495, 231-262).  Returns the chosen
- * triangle index; p = v0 + a1*u + a2*v. */
+ * primitive id; a triangle gives p = v0 + a1*u + a2*v.  Sphere lights (d8 policy) enter the
+ * CDF with area 4*3.14159*r^2 and give the uniform point c + r*(sqrt(1-z^2)cos(phi),
+ * sqrt(1-z^2)sin(phi), z), z = 1 - 2u, phi = 2*3.14159*v -- the same three draws. */
 static int32_t pick_light(const or_scene* sc, or_xorwow* rng, or_vec3* p_out)
 {
     float rand_area = sc->total_light_area * or_uniform(rng);
     int32_t sel = 0;
     for (uint32_t j = 0; j < sc->num_lights; ++j) {
-        const or_tri* lt = sc->tris + sc->lights[j];
-        or_vec3 a1 = vsub(sc->verts[lt->v1], sc->verts[lt->v0]);
-        or_vec3 a2 = vsub(sc->verts[lt->v2], sc->verts[lt->v0]);
-        float area = vlength(vcross(a1, a2)) / 2;
-        if (rand_area < area && rand_area > 0) sel = (int32_t)sc->lights[j];
+        const uint32_t e = sc->lights[j];
+        float area;
+        int32_t id;
+        if (e & OR_LIGHT_SPHERE) {
+            area = sphere_area(sc->spheres[e ^ OR_LIGHT_SPHERE].rad);
+            id = (int32_t)(sc->num_tris + (e ^ OR_LIGHT_SPHERE));
+        } else {
+            const or_tri* lt = sc->tris + e;
+            or_vec3 a1 = vsub(sc->verts[lt->v1], sc->verts[lt->v0]);
+            or_vec3 a2 = vsub(sc->verts[lt->v2], sc->verts[lt->v0]);
+            area = vlength(vcross(a1, a2)) / 2;
+            id = (int32_t)e;
+        }
+        if (rand_area < area && rand_area > 0) sel = id;
         rand_area -= area;
     }
     float u = or_uniform(rng);
     float v = or_uniform(rng);
+    if ((uint32_t)sel >= sc->num_tris) {
+        const or_sphere* s = sc->spheres + ((uint32_t)sel - sc->num_tris);
+        float z = 1.0f - 2.0f * u;
+        float rxy = sqrtf(fmax_f(0.0f, 1.0f - z * z));
+        float phi = (float)(2 * 3.14159 * (double)v);
+        float si, co;
+        or_sincos(phi, &si, &co);
+        *p_out = vadd(s->pos, vmul(v3(rxy * co, rxy * si, z), s->rad));
+        return sel;
+    }
     const or_tri* st = sc->tris + sel;
     or_vec3 v0 = sc->verts[st->v0];
     or_vec3 a1 = vsub(sc->verts[st->v1], v0);
@@ -421,12 +485,11 @@ void or_radiance_unidir(const or_scene* sc, or_vec3 o, or_vec3 dir, int bounces,
         t = (float)((double)t - 0.001);                           /* :431 */
         if ((double)t < 0.001) weight = c3(0, 0, 0);               /* :432-435 */
         if (t > OR_MAX_FLOAT - 1) { weight = c3(0, 0, 0); tri = 0; t = 0; }   /* :436-441 */
-        const or_tri* ct = sc->tris + tri;
-        const or_mat* cm = sc->mats + ct->mat;
-        or_vec3 normal = ct->norm;
+        or_vec3 pos = vadd(o, vmul(dir, t));                      /* :449 */
+        const or_mat* cm = mat_ptr(sc, prim_mat(sc, tri));
+        or_vec3 normal = prim_normal(sc, tri, pos);
         or_vec3 odir = vmul(dir, -1);
         or_vec3 ldir;
-        or_vec3 pos = vadd(o, vmul(dir, t));                      /* :449 */
         if (cm->emission[0] != 0) {                               /* :453-457 */
             accum = cadd(accum, cmul(weight, mat_emission(cm)));
             weight = c3(0, 0, 0);
@@ -478,10 +541,10 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
     {
         or_vec3 p;
         int32_t sel = pick_light(sc, rng, &p);
-        or_vec3 normal = sc->tris[sel].norm;
+        or_vec3 normal = prim_normal(sc, sel, p);
         x[0] = vadd(p, vmul(normal, 0.001f));
         norm[0] = normal;
-        mat[0] = sc->tris[sel].mat;
+        mat[0] = prim_mat(sc, sel);
         inv_prob[0] = sc->total_light_area;
     }
     /* light bounce (:271-301) */
@@ -491,10 +554,10 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
         or_trace(sc, x[0], odir, &tri, &t, cnt);
         t = (float)((double)t - 0.001);
         if (t > OR_MAX_FLOAT - 1) { tri = 0; t = 0; }
-        or_vec3 n2 = sc->tris[tri].norm;
         or_vec3 pos = vadd(x[0], vmul(odir, t));
+        or_vec3 n2 = prim_normal(sc, tri, pos);
         float G = fabsf(vdot(n2, odir)) / fmax_f(0.001f, t * t);
-        x[1] = pos; norm[1] = n2; mat[1] = sc->tris[tri].mat;
+        x[1] = pos; norm[1] = n2; mat[1] = prim_mat(sc, tri);
         inv_prob[1] = (float)(2 * 3.14159 / (double)G);
     }
     /* camera vertex (:304-308) */
@@ -506,8 +569,8 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
         t = (float)((double)t - 0.001);
         if (t > OR_MAX_FLOAT - 1) { tri = 0; t = 0; }
         x[3] = vadd(cam_o, vmul(cam_d, t));
-        norm[3] = sc->tris[tri].norm;
-        mat[3] = sc->tris[tri].mat;
+        norm[3] = prim_normal(sc, tri, x[3]);
+        mat[3] = prim_mat(sc, tri);
         inv_prob[3] = 1;
     }
     /* camera second hit (:332-350) */
@@ -517,29 +580,29 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
         or_trace(sc, x[3], d, &tri, &t, cnt);
         t = (float)((double)t - 0.001);
         if (t > OR_MAX_FLOAT - 1 || tri < 0) { tri = 0; t = 0; }    /* d2 */
-        or_vec3 n = sc->tris[tri].norm;
+        x[2] = vadd(x[3], vmul(d, t));
+        or_vec3 n = prim_normal(sc, tri, x[2]);
         float G = fabsf(vdot(norm[3], d) * vdot(n, d)) / (t * t);
         if (G == 0) G = 1;
         if (G != G) G = 1;
-        x[2] = vadd(x[3], vmul(d, t));
         norm[2] = n;
-        mat[2] = sc->tris[tri].mat;
+        mat[2] = prim_mat(sc, tri);
         inv_prob[2] = (float)(3.14159 / (double)G);
     }
     /* connections (:352-412) */
     col accum = c3(0, 0, 0);
-    col le = mat_emission(sc->mats + mat[0]);
+    col le = mat_emission(mat_ptr(sc, mat[0]));
     for (int i = 0; i < 2; ++i) {
         for (int j = 2; j < 4; ++j) {
             col w = cmulf(le, inv_prob[0]);
             for (int k = 1; k <= i; ++k) {
                 float G = geo_term(x[k], x[k - 1], norm[k], norm[k - 1]);
-                col fs = cdivf(mat_albedo(sc->mats + mat[k]), 3.14159f);
+                col fs = cdivf(mat_albedo(mat_ptr(sc, mat[k])), 3.14159f);
                 w = cmulf(cmulf(cmul(w, fs), G), inv_prob[k]);
             }
             for (int k = j + 1; k < 4; ++k) {
                 float G = geo_term(x[k], x[k - 1], norm[k], norm[k - 1]);
-                col fs = cdivf(mat_albedo(sc->mats + mat[k]), 3.14159f);
+                col fs = cdivf(mat_albedo(mat_ptr(sc, mat[k])), 3.14159f);
                 w = cmulf(cmulf(cmul(w, fs), G), inv_prob[k]);
             }
             {
@@ -548,7 +611,7 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
                 or_vec3 ray = vnormalized(seg);
                 float G = fmax_f(0.0f, vdot(ray, norm[j]) * vdot(vmul(ray, -1), norm[i])) / vdot(seg, seg);
                 if (G != G) G = 0;
-                col fs = cdivf(mat_albedo(sc->mats + mat[j]), 3.14159f);
+                col fs = cdivf(mat_albedo(mat_ptr(sc, mat[j])), 3.14159f);
                 w = cmulf(cmulf(cmul(w, fs), G), inv_prob[j]);
                 float m = (float)fmax(w.r, fmax(w.g, w.b));
                 float V = 0;
@@ -560,7 +623,7 @@ void or_radiance_head(const or_scene* sc, or_vec3 cam_o, or_vec3 cam_d,
                 w = cmulf(w, V);
             }
             accum = cadd(accum, w);
-            accum = cadd(accum, mat_emission(sc->mats + mat[3]));
+            accum = cadd(accum, mat_emission(mat_ptr(sc, mat[3])));
         }
     }
     out[0] = accum.r; out[1] = accum.g; out[2] = accum.b;

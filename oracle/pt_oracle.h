@@ -46,6 +46,10 @@ typedef struct {                                                   /* camera.h:2
     int32_t pxl_width, pxl_height;
 } or_camera;
 typedef struct { uint32_t d; uint32_t v[5]; } or_xorwow;          /* curandStateXORWOW d, v[5] */
+/* sphere.h:7-12; the tail {diffuse, emission} has or_mat's layout.  Semantics are the build's
+ * (reference has none): see or_sphere_t, prim_normal, pick_light. */
+typedef struct { or_vec3 pos; float rad; double diffuse[3]; double emission[3]; } or_sphere;
+#define OR_LIGHT_SPHERE 0x80000000u   /* lights[] entry of an emissive sphere */
 
 typedef struct {                                                   /* modelLoader.h:29-41 + BVH.h:116-121 */
     uint32_t num_verts, num_tris, num_mats, num_lights;
@@ -55,7 +59,9 @@ typedef struct {                                                   /* modelLoade
     const uint32_t* lights;
     float total_light_area;
     const or_node* bvh;
-    uint32_t bvh_size;
+    uint32_t bvh_size;             /* 0: no triangles (a scene of spheres)                     */
+    const or_sphere* spheres;      /* hit ids num_tris + i; material handles num_mats + i        */
+    uint32_t num_spheres;
 } or_scene;
 
 typedef struct {
@@ -81,6 +87,7 @@ void     or_camera_ray(const or_camera* cam, uint32_t idx, float u1, float u2, o
 
 /* ---- traversal (kernel.cu:112-161); returns 0, or -1 on stack overflow */
 int      or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri, float* t, or_counters* cnt);
+float    or_sphere_t(or_vec3 o, or_vec3 d, const or_sphere* s);   /* MAX_FLOAT on a miss */
 /* or_trace over rays[6n] = {o.xyz, d.xyz} (OpenMP); returns the number of stack overflows. */
 int      or_trace_batch(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t);
 
