@@ -320,20 +320,40 @@ __device__ __forceinline__ void pin(uint4& v)
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
-// triIntersect (modelLoader.h:49-83) on a record already in registers; kMk: one IEEE
-// reciprocal of `a`, Markstein quotients.
+// The smallest float whose double is >= 0.00001: for float a, (double)a < 0.00001 <=> a < kTriEps.
+constexpr float kTriEps = 0x1.4f8b5ap-17f;
+
+// RN(1/a) for kTriEps <= |a| <= 2^64 from the hardware reciprocal and one Newton step:
+// verified equal to IEEE 1.0f / a for every float of that range, both signs, on gfx950
+// (tools/gpu/rcp_check.hip; DESIGN.md "Exact division").  |a| is at most ~2^43 in a scene that
+// passes the Markstein preconditions (coordinates <= 2^20, unit-scale directions).
+__device__ __forceinline__ float rcp_rn(float a)
+{
+    const float y0 = __builtin_amdgcn_rcpf(a);
+    const float e = __builtin_fmaf(-a, y0, 1.0f);
+    return __builtin_fmaf(e, y0, y0);
+}
+// div_mk for a divisor known to be nonzero
+__device__ __forceinline__ float div_mk_nz(float x, float d, float y)
+{
+    const float q0 = x * y;
+    return __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
+}
+
+// triIntersect (modelLoader.h:49-83) on a record already in registers; kMk: RN(1/a) and
+// Markstein quotients.
 template <bool kMk>
 __device__ __forceinline__ float tri_hit_rec(V3 o, V3 d, float4 A, float4 B, float4 C)
 {
     const V3 v0 = v3(A.x, A.y, A.z), e1 = v3(A.w, B.x, B.y), e2 = v3(B.z, B.w, C.x);
     const V3 q = cross(d, e2);
     const float a = dot(e1, q);
-    if ((double)__builtin_fabsf(a) < 0.00001) return kMaxFloat;
+    if (__builtin_fabsf(a) < kTriEps) return kMaxFloat;   // == (double)|a| < 0.00001, NaN included
     const V3 w = o - v0;
     V3 s;
     if (kMk) {
-        const float ya = 1.0f / a;
-        s = v3(div_mk(w.x, a, ya), div_mk(w.y, a, ya), div_mk(w.z, a, ya));
+        const float ya = rcp_rn(a);
+        s = v3(div_mk_nz(w.x, a, ya), div_mk_nz(w.y, a, ya), div_mk_nz(w.z, a, ya));
     } else {
         s = w / a;
     }
@@ -397,6 +417,7 @@ struct W4 {
     int32_t lsp;         // leaves queued in the LDS leaf ring (besides `leaf`)
     float best_t;
     uint32_t best_slot;  // render-path triangle slot of the best hit, kNone = none
+    uint32_t nx, ny, nz; // byte offsets in DNode4 of the near plane per axis (lo, or hi for inv < 0)
 };
 
 // The exact reference test a winner must pass (DESIGN.md "Traversal" 2): the reference slab test
@@ -433,6 +454,9 @@ __device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root
     if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, w.inv.y);
     if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, w.inv.z);
     w.oi = v3(o.x * w.inv.x, o.y * w.inv.y, o.z * w.inv.z);
+    w.nx = (w.inv.x < 0.0f) ? 48u : 0u;    // hix : lox  (the far plane is at nx ^ 48)
+    w.ny = (w.inv.y < 0.0f) ? 64u : 16u;   // hiy : loy  (ny ^ 80)
+    w.nz = (w.inv.z < 0.0f) ? 80u : 32u;   // hiz : loz  (nz ^ 112)
     w.node = 0; w.leaf = kNone; w.sp = 0; w.lsp = 0;
     w.best_t = kMaxFloat; w.best_slot = kNone;
     // conservative root test (boxes inflated; NaN planes are ignored by min/max)
@@ -444,17 +468,43 @@ __device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root
     return !(tn > tf) && !(tf < -cull_abs);
 }
 
-// Conservative 4-box test; returns entry distances (+inf = not entered).
-__device__ __forceinline__ float box_enter(const W4& w, float lx, float ly, float lz, float hx, float hy, float hz,
-                                           float limit, float cull_abs)
+// Conservative test of two child boxes (packed: one v_pk_fma_f32 per plane pair).  The near /
+// far planes were picked per ray by the load offsets, so t_near <= t_far per axis already (FMA
+// rounding is monotonic and lo <= hi): the entry is max3 of the near values, the exit min3 of the
+// far ones, and no NaN can arise (finite bounds, |inv| <= 2^100).  Returns max(entry, -cull_abs)
+// (+inf = not entered): the box is entered iff max(entry, -cull_abs) <= min(exit, limit), which is
+// entry <= exit && exit >= -cull_abs && entry <= limit.  Entries below -cull_abs only sort first.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, float b, float c)
 {
-    const float x0 = __builtin_fmaf(lx, w.inv.x, -w.oi.x), x1 = __builtin_fmaf(hx, w.inv.x, -w.oi.x);
-    const float y0 = __builtin_fmaf(ly, w.inv.y, -w.oi.y), y1 = __builtin_fmaf(hy, w.inv.y, -w.oi.y);
-    const float z0 = __builtin_fmaf(lz, w.inv.z, -w.oi.z), z1 = __builtin_fmaf(hz, w.inv.z, -w.oi.z);
-    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)), __builtin_fminf(z0, z1));
-    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)), __builtin_fmaxf(z0, z1));
-    const bool in = !(tn > tf) && !(tf < -cull_abs) && !(tn > limit);
-    return in ? tn : INFINITY;
+    return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
+}
+__device__ __forceinline__ void box_enter2(const W4& w, f2 nx, f2 ny, f2 nz, f2 fx, f2 fy, f2 fz, float limit,
+                                           float ncull, float& t0, float& t1)
+{
+    const f2 ax = pk_fma(nx, w.inv.x, -w.oi.x), ay = pk_fma(ny, w.inv.y, -w.oi.y), az = pk_fma(nz, w.inv.z, -w.oi.z);
+    const f2 bx = pk_fma(fx, w.inv.x, -w.oi.x), by = pk_fma(fy, w.inv.y, -w.oi.y), bz = pk_fma(fz, w.inv.z, -w.oi.z);
+    const float n0 = __builtin_fmaxf(__builtin_fmaxf(ax.x, ay.x), __builtin_fmaxf(az.x, ncull));
+    const float n1 = __builtin_fmaxf(__builtin_fmaxf(ax.y, ay.y), __builtin_fmaxf(az.y, ncull));
+    const float f0 = __builtin_fminf(__builtin_fminf(bx.x, by.x), __builtin_fminf(bz.x, limit));
+    const float f1 = __builtin_fminf(__builtin_fminf(bx.y, by.y), __builtin_fminf(bz.y, limit));
+    t0 = (n0 <= f0) ? n0 : INFINITY;
+    t1 = (n1 <= f1) ? n1 : INFINITY;
+}
+// x * 48 as (x << 5) + (x << 4): two full-rate ops instead of a quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t mul48(uint32_t x)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(x), "v"(x << 4));
+    return r;
+}
+__device__ __forceinline__ float4 ld_f4(const void* base, uint32_t off)
+{
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
+}
+__device__ __forceinline__ uint4 ld_u4(const void* base, uint32_t off)
+{
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + off);
 }
 
 __device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32_t& rb)
@@ -503,11 +553,15 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
 {
     const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 4);
     const bool leaf = w.leaf != kNone;
-    const DTri* tr = tris + (leaf ? w.leaf : 0u);
-    float4 A = tr->a, B = tr->b, C = tr->c;
-    const DNode4* nd = nodes + (visit ? w.node : 0u);
-    float4 lx = nd->lox, ly = nd->loy, lz = nd->loz, hx = nd->hix, hy = nd->hiy, hz = nd->hiz;
-    uint4 ch = nd->child;
+    // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
+    const uint32_t tb = mul48(leaf ? w.leaf : 0u);
+    float4 A = ld_f4(tris, tb), B = ld_f4(tris, tb + 16u), C = ld_f4(tris, tb + 32u);
+    const uint32_t nb = (visit ? w.node : 0u) * 128u;
+    const uint32_t ox = nb | w.nx, oy = nb | w.ny, oz = nb | w.nz;
+    const float4 NX = ld_f4(nodes, ox), FX = ld_f4(nodes, ox ^ 48u);
+    const float4 NY = ld_f4(nodes, oy), FY = ld_f4(nodes, oy ^ 80u);
+    const float4 NZ = ld_f4(nodes, oz), FZ = ld_f4(nodes, oz ^ 112u);
+    uint4 ch = ld_u4(nodes, nb + 96u);
     pin(A); pin(B); pin(C);   // (the node's fields feed unconditional tests: no pin needed)
     if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
@@ -522,12 +576,13 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         w.leaf = kNone;
     }
     if (visit) {
-        float lim = w.best_t * cull_rel;
+        const float lim = w.best_t * cull_rel;
         // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
-        float t0 = box_enter(w, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, lim, cull_abs);
-        float t1 = box_enter(w, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, lim, cull_abs);
-        float t2 = box_enter(w, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, lim, cull_abs);
-        float t3 = box_enter(w, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, lim, cull_abs);
+        float t0, t1, t2, t3;
+        box_enter2(w, f2{NX.x, NX.y}, f2{NY.x, NY.y}, f2{NZ.x, NZ.y}, f2{FX.x, FX.y}, f2{FY.x, FY.y}, f2{FZ.x, FZ.y},
+                   lim, -cull_abs, t0, t1);
+        box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
+                   lim, -cull_abs, t2, t3);
         uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
         auto queue = [&](uint32_t slot) {
             if (w.leaf == kNone) { w.leaf = slot; return; }

@@ -1430,6 +1430,10 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     std::vector<float> tone(256);
     c->tone_ok = pt::tonemap_thresholds(tone.data());
 
+    // the BVH4 walk addresses nodes and triangle records by 32-bit byte offsets (pt_device.h
+    // walk4_step): larger structures take the exact reference-BVH walk for every ray
+    if ((uint64_t)an.size() * sizeof(an[0]) >= (1ull << 32) || (uint64_t)at.size() * sizeof(at[0]) >= (1ull << 32))
+        c->scene_fast = false;
     int rc = PT_OK;
     lap("records + jump/tone tables");
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
