@@ -274,7 +274,7 @@ __device__ __forceinline__ bool coord_ok(float v)
 __device__ __forceinline__ bool dir_ok(float v)
 {
     const float a = __builtin_fabsf(v);
-    return a == 0.0f || a >= 0x1p-100f;
+    return a == 0.0f || (a >= 0x1p-100f && a <= 0x1p45f);
 }
 
 __device__ __forceinline__ bool ray_fast(V3 o, V3 d)
@@ -323,15 +323,21 @@ __device__ __forceinline__ void pin(uint4& v)
 // The smallest float whose double is >= 0.00001: for float a, (double)a < 0.00001 <=> a < kTriEps.
 constexpr float kTriEps = 0x1.4f8b5ap-17f;
 
-// RN(1/a) for kTriEps <= |a| <= 2^64 from the hardware reciprocal and one Newton step:
+// RN(1/a) for 2^-100 <= |a| <= 2^100 from the hardware reciprocal and one Newton step:
 // verified equal to IEEE 1.0f / a for every float of that range, both signs, on gfx950
-// (tools/gpu/rcp_check.hip; DESIGN.md "Exact division").  |a| is at most ~2^43 in a scene that
-// passes the Markstein preconditions (coordinates <= 2^20, unit-scale directions).
+// (tools/gpu/rcp_check.hip; DESIGN.md "Exact division").  Under the Markstein preconditions
+// (coordinates <= 2^20, 2^-100 <= |d_k| <= 2^45) every divisor lies in it: direction
+// components, and triangle determinants kTriEps <= |a| <= ~2^88.
 __device__ __forceinline__ float rcp_rn(float a)
 {
     const float y0 = __builtin_amdgcn_rcpf(a);
     const float e = __builtin_fmaf(-a, y0, 1.0f);
     return __builtin_fmaf(e, y0, y0);
+}
+// IEEE 1/d for d = 0 (+-inf) or 2^-100 <= |d| <= 2^100
+__device__ __forceinline__ float rcp_or_inf(float d)
+{
+    return (d == 0.0f) ? __builtin_copysignf(INFINITY, d) : rcp_rn(d);
 }
 // div_mk for a divisor known to be nonzero
 __device__ __forceinline__ float div_mk_nz(float x, float d, float y)
@@ -427,7 +433,7 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
                                            const RNode* __restrict__ rnodes, const uint32_t* __restrict__ rparent)
 {
     const bool zero_dir = d.x == 0.0f || d.y == 0.0f || d.z == 0.0f;
-    const V3 y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // IEEE reciprocals: div_mk's y
+    const V3 y = v3(rcp_or_inf(d.x), rcp_or_inf(d.y), rcp_or_inf(d.z));   // == IEEE 1/d: div_mk's y
     uint32_t n = parent;
     for (;;) {
         const RNode* p = rnodes + n;
@@ -440,25 +446,35 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
     }
 }
 
-// Only rays satisfying ray_fast() walk the BVH4 (all exact tests use Markstein quotients);
-// the others take trace_slow() below.
-__device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root, float cull_abs)
+// walk4_begin in two halves: the ray-independent reset, and the per-ray reciprocals / plane
+// offsets (the path-pool kernel runs the latter after the first node fetch is in flight).
+__device__ __forceinline__ void walk4_reset(W4& w)
+{
+    w.node = 0; w.leaf = kNone; w.sp = 0; w.lsp = 0;
+    w.best_t = kMaxFloat; w.best_slot = kNone;
+}
+__device__ __forceinline__ void walk4_setup(W4& w, V3 o, V3 d)
 {
     // Conservative slab values are lo*inv - o*inv (one FMA).  A zero component would make that
     // inf - inf = NaN on one plane and -inf on the other, which min/max cannot repair, so the
     // reciprocal is clamped to +-2^100: o*inv stays finite (|o| <= 2^20), and the inflated boxes
     // keep every plane >= margin from an origin inside the true slab, so the signs -- hence
     // "inside: unbounded, outside: rejected" -- come out right.  Exact tests use 1/d itself.
-    w.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    if (d.x == 0.0f) w.inv.x = __builtin_copysignf(0x1p100f, w.inv.x);
-    if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, w.inv.y);
-    if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, w.inv.z);
+    w.inv = v3(rcp_rn(d.x), rcp_rn(d.y), rcp_rn(d.z));   // ray_fast: d_k is 0 or in rcp_rn's range
+    if (d.x == 0.0f) w.inv.x = __builtin_copysignf(0x1p100f, d.x);   // (1/+-0 = +-inf: same sign as d)
+    if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, d.y);
+    if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, d.z);
     w.oi = v3(o.x * w.inv.x, o.y * w.inv.y, o.z * w.inv.z);
     w.nx = (w.inv.x < 0.0f) ? 48u : 0u;    // hix : lox  (the far plane is at nx ^ 48)
     w.ny = (w.inv.y < 0.0f) ? 64u : 16u;   // hiy : loy  (ny ^ 80)
     w.nz = (w.inv.z < 0.0f) ? 80u : 32u;   // hiz : loz  (nz ^ 112)
-    w.node = 0; w.leaf = kNone; w.sp = 0; w.lsp = 0;
-    w.best_t = kMaxFloat; w.best_slot = kNone;
+}
+// Only rays satisfying ray_fast() walk the BVH4 (all exact tests use Markstein quotients);
+// the others take trace_slow() below.  Returns the conservative root test.
+__device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root, float cull_abs)
+{
+    walk4_setup(w, o, d);
+    walk4_reset(w);
     // conservative root test (boxes inflated; NaN planes are ignored by min/max)
     const float x0 = __builtin_fmaf(root[0], w.inv.x, -w.oi.x), x1 = __builtin_fmaf(root[3], w.inv.x, -w.oi.x);
     const float y0 = __builtin_fmaf(root[1], w.inv.y, -w.oi.y), y1 = __builtin_fmaf(root[4], w.inv.y, -w.oi.y);
@@ -546,10 +562,16 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 // later steps, overlapped with later node fetches), inner children are visited near-first.
 // Deferring a leaf test only delays best_t improvements, i.e. culls less: the result is the
 // same exact minimum.  A node is visited only while the leaf queue has room for its children.
-template <bool kCount>
+// `setup(w)` runs once the step's fetches are issued (the pool kernel fetches a new ray there and
+// runs walk4_setup, so the ray's round trip overlaps the root node's).
+struct NoSetup {
+    __device__ void operator()(W4&) const {}
+};
+template <bool kCount, class Setup = NoSetup>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
-                                           float cull_abs, uint32_t node_mask, Counters& cnt)
+                                           float cull_abs, uint32_t node_mask, Counters& cnt,
+                                           const Setup& setup = Setup())
 {
     const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 4);
     const bool leaf = w.leaf != kNone;
@@ -562,6 +584,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const float4 NY = ld_f4(nodes, oy), FY = ld_f4(nodes, oy ^ 80u);
     const float4 NZ = ld_f4(nodes, oz), FZ = ld_f4(nodes, oz ^ 112u);
     uint4 ch = ld_u4(nodes, nb + 96u);
+    setup(w);
     pin(A); pin(B); pin(C);   // (the node's fields feed unconditional tests: no pin needed)
     if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {

@@ -58,6 +58,9 @@ struct Args {
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
     uint32_t* spill;                // LDS-stack overflow, entry k of lane g at spill[(k-kRing)*stride + g]
     uint32_t spill_stride;
+    uint32_t cold_stride;           // records of the cold array (lanes, or paths of the pool kernel)
+    float4* pray;                   // pool kernel: path g's ray and pending hit at pray[2g], pray[2g+1]:
+                                    // (o.x, o.y, o.z, d.x), (d.y, d.z, hit slot / id, hit t)
     float acc_root[6];
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
     const uint32_t* pix_states;     // XORWOW v0..v4, d of each work unit, word k of unit u at [k*nunits + u]
@@ -528,12 +531,15 @@ enum : int {
     CW_WGT = 25,                      // wgt (f64 x 3)
     CW_NEND = 31,                     // last sample number of the unit
     CW_Q = 32,                        // pixel slot of the unit (per-sample buffer row)
-    kColdWords = 33
+    CW_PST = 33,                      // path-pool kernel: path state (ST_*) while queued for shading
+    CW_CD = 34,                       // camera ray direction of a pinhole unit (f32 x 3, CF_CAMC)
+    kColdWords = 37
 };
 // CF_OWNER: chunk 0 of a split pixel (publishes its primary hit in pmemo); CF_SHARE: a later
 // chunk (takes the published hit instead of tracing the camera ray again)
 // CF_MEMO: the pending hit came from the memo (already includes spheres)
-enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32 };
+// CF_CAMC: the (sample-invariant, pinhole) camera direction is cached in CW_CD
+enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64 };
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the word
 // offset k * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -655,6 +661,232 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
     if (lane == __ffsll((long long)m) - 1) atomicAdd(c, (unsigned long long)__popcll(m));
 }
 
+// The shading half of the wavefront state machine, for the lanes that are not tracing: consume
+// the pending hit (winner check; exact slow walk when needed), run bounces, finish and start
+// samples until the lane needs a trace or its unit is done, then give finished lanes new units.
+// On return the lane's state is ST_TRACE (w set up for its ray), ST_SHADE / ST_SLOW (shading
+// pending: a memo hit, a root miss or a slow ray right after a refill) or ST_DONE.
+__device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
+                                           int32_t& htri, float& ht, W4& w, const Stack4& S,
+                                           unsigned long long* lcnt)
+{
+    const int D = a.bounces;
+    if (state == ST_CHECK) {
+        // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
+        // (rare), the exact reference-BVH walk redoes the ray
+        const float4 C = a.acc_tris[htri].c;
+        htri = (int32_t)__float_as_uint(C.y);
+        state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
+    }
+    int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
+    uint32_t fl = R.ld(CW_FLAGS);
+    Rng rng;
+    rng.d = R.ld(CW_RNG); rng.v0 = R.ld(CW_RNG + 1); rng.v1 = R.ld(CW_RNG + 2);
+    rng.v2 = R.ld(CW_RNG + 3); rng.v3 = R.ld(CW_RNG + 4); rng.v4 = R.ld(CW_RNG + 5);
+    C3 wgt = c3(R.ldd(CW_WGT), R.ldd(CW_WGT + 2), R.ldd(CW_WGT + 4));
+
+    // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
+    // a ray outside the Markstein preconditions, which takes the exact slow walk)
+    auto begin_trace = [&](V3 o, V3 d) -> bool {
+        wave_count(lcnt + 0, lane);
+        if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }   // spheres only
+        if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
+        if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
+            htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
+        }
+        state = ST_TRACE;
+        return false;
+    };
+    // start sample n of pixel (px, py): camera ray, then memo or trace
+    auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
+        i = 0;
+        R.std_(CW_ACC, 0.0); R.std_(CW_ACC + 2, 0.0); R.std_(CW_ACC + 4, 0.0);
+        wgt = c3(1, 1, 1);
+        float u1 = 0.0f, u2 = 0.0f;
+        const bool lens = (fl & CF_LENS) != 0u;
+        if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
+        if (lens || !(fl & CF_CAMC)) {
+            camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
+            if (!lens) {   // a pinhole ray is the same for every sample of the pixel
+                R.st(CW_CD, __float_as_uint(rd.x)); R.st(CW_CD + 1, __float_as_uint(rd.y)); R.st(CW_CD + 2, __float_as_uint(rd.z));
+                fl |= CF_CAMC;
+            }
+        } else {
+            ro = v3(0.0f, 0.0f, 0.0f) + v3(a.cam.pos[0], a.cam.pos[1], a.cam.pos[2]);   // as camera_ray forms it
+            rd = v3(__uint_as_float(R.ld(CW_CD)), __uint_as_float(R.ld(CW_CD + 1)), __uint_as_float(R.ld(CW_CD + 2)));
+        }
+        wave_count(lcnt + 1, lane);
+        if (fl & CF_HAVE) {
+            htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
+            fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
+            return true;
+        }
+        if (fl & CF_SHARE) {
+            // the pixel's chunk 0 may have published the (sample-invariant) primary hit
+            const uint32_t q = R.ld(CW_Q);
+            const uint32_t tv = __hip_atomic_load(a.pmemo + 2 * (size_t)q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tv != 0u) {
+                htri = (int32_t)(tv - 2u);
+                ht = __uint_as_float(a.pmemo[2 * (size_t)q + 1]);
+                fl = (fl | CF_PRIMARY | CF_MEMO) & ~CF_SHARE;   // stores the unit memo on shading
+                state = ST_SHADE;
+                return true;
+            }
+        }
+        fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
+        return begin_trace(ro, rd);
+    };
+
+    bool again = (state == ST_SHADE || state == ST_SLOW);
+    while (again) {
+        again = false;
+        if (state == ST_SLOW) {
+            wave_count(lcnt + 3, lane);
+            trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
+                       &htri, &ht);
+        }
+        state = ST_SHADE;
+        if (a.num_spheres && !(fl & CF_MEMO)) apply_spheres(a, ro, rd, &htri, &ht);
+        fl &= ~CF_MEMO;
+        if (fl & CF_PRIMARY) {
+            fl = (fl | CF_HAVE) & ~CF_PRIMARY;
+            R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
+            if (fl & CF_OWNER) {
+                const uint32_t q = R.ld(CW_Q);
+                a.pmemo[2 * (size_t)q + 1] = __float_as_uint(ht);
+                __hip_atomic_store(a.pmemo + 2 * (size_t)q, (uint32_t)(htri + 2), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                fl &= ~CF_OWNER;
+            }
+        }
+        // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
+        {
+            int32_t tri = htri;
+            float t = (float)((double)ht - 0.001);
+            if ((double)t < 0.001) wgt = c3(0, 0, 0);
+            if (t > kMaxFloat - 1) { wgt = c3(0, 0, 0); tri = 0; t = 0; }
+            const V3 pos = ro + rd * t;
+            const DMat* cm = a.mats + prim_mat(a, tri);
+            const V3 normal = prim_normal(a, tri, pos);
+            if (cm->emission[0] != 0) {
+                C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
+                acc = cadd(acc, cmul(wgt, mat_emission(cm)));
+                R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
+                wgt = c3(0, 0, 0);
+            }
+            V3 ldir;
+            const float u = rng_uniform(rng);
+            if (u < 0.5) {
+                ldir = cosine_ray(normal, rng);
+                wgt = cmul(wgt, cmulf(brdf(cm), (float)3.14159));
+            } else {
+                V3 p1;
+                pick_light(a, rng, &p1);
+                const V3 dd = p1 - pos;
+                ldir = normalized(dd);
+                const float cos_l = __builtin_fmaxf(0.0f, dot(ldir, normal));
+                const float cos_o = __builtin_fmaxf(0.0f, dot(v3(0, -1, 0), ldir * -1));
+                const float G = cos_l * cos_o / dot(dd, dd);
+                wgt = cmul(wgt, cmulf(cmulf(brdf(cm), G), a.total_light_area));
+                i = (i > D - 2) ? i : D - 2;
+            }
+            ro = pos;
+            rd = ldir;
+            ++i;
+        }
+        // advance to the next trace this lane needs
+        for (;;) {
+            if (i >= D) {
+                wave_count(lcnt + 2, lane);
+                const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
+                if (a.chunks == 1) {
+                    const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
+                    const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
+                    const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
+                    const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
+                    if (n >= a.spp) {
+                        float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+                        o3[0] = (float)m0;
+                        o3[1] = (float)m1;
+                        o3[2] = (float)m2;
+                        state = ST_IDLE;
+                        break;
+                    }
+                    R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
+                } else {
+                    // split pixel: keep L_n, finalize_pixels forms the ordered mean
+                    const size_t ch = (size_t)a.spp * a.npix;
+                    double* L = a.lbuf + (size_t)(n - 1) * a.npix + R.ld(CW_Q);
+                    L[0] = R.ldd(CW_ACC);
+                    L[ch] = R.ldd(CW_ACC + 2);
+                    L[2 * ch] = R.ldd(CW_ACC + 4);
+                    if ((uint32_t)n >= R.ld(CW_NEND)) {
+                        state = ST_IDLE;
+                        break;
+                    }
+                }
+                ++n;
+                again = start_sample(px, py);
+                break;
+            }
+            if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
+                wave_count(lcnt + 1, lane);
+                const float u = rng_uniform(rng);
+                if (u < 0.5) { rng_next(rng); rng_next(rng); }
+                else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
+                ++i;
+                continue;
+            }
+            wave_count(lcnt + 1, lane);
+            again = begin_trace(ro, rd);
+            break;
+        }
+    }
+
+    // refill: lanes whose pixel is finished take the next pixels of this shard
+    const uint64_t idle = __ballot(state == ST_IDLE);
+    if (idle) {
+        const uint32_t need = (uint32_t)__popcll(idle);
+        const int leader = __ffsll((long long)idle) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(a.pixel_counter, need);
+        base = __shfl(base, leader, 64);
+        if (state == ST_IDLE) {
+            const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            if (u >= a.nunits) {
+                state = ST_DONE;
+            } else {
+                const uint32_t c = u / a.npix, q = u - c * a.npix;
+                uint32_t px, py;
+                if (unit_pixel(a, q, &px, &py)) {
+                    const uint32_t idx = morton2(px, py);
+                    // curand_init's state, computed for every unit by init_pixel_states
+                    rng.d = a.pix_states[5 * (size_t)a.nunits + u];
+                    rng.v0 = a.pix_states[u];
+                    rng.v1 = a.pix_states[(size_t)a.nunits + u];
+                    rng.v2 = a.pix_states[2 * (size_t)a.nunits + u];
+                    rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
+                    rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
+                    fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
+                    if (a.chunks > 1 && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
+                        fl |= (c == 0) ? CF_OWNER : CF_SHARE;
+                    n = (int)chunk_first(a, c) + 1;
+                    R.st(CW_PX, px); R.st(CW_PY, py);
+                    R.st(CW_NEND, chunk_first(a, c + 1));
+                    R.st(CW_Q, q);
+                    R.std_(CW_M, 0.0); R.std_(CW_M + 2, 0.0); R.std_(CW_M + 4, 0.0);
+                    start_sample(px, py);
+                }
+            }
+        }
+    }
+
+    R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i); R.st(CW_FLAGS, fl);
+    R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
+    R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
+    R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
+}
+
 template <bool kCount, int kMinWaves>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
@@ -665,7 +897,6 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int D = a.bounces;
     Counters cnt;
     cnt.nodes = 0;
     cnt.tris = 0;
@@ -683,8 +914,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.ring = lds_wf + (threadIdx.x >> 6) * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
     S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.spill_stride * 4u), 0x00020000),
-                    (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.spill_stride * 4u};
+    const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
+                    (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.cold_stride * 4u};
 
     for (;;) {
         // ---------------------------------------------------------------- walk
@@ -717,215 +948,210 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // index, bounce, flags, RNG, path weight); accumulator, running mean, pixel and memo
         // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
-        if (state != ST_TRACE && state != ST_DONE) {
-            if (state == ST_CHECK) {
-                // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
-                // (rare), the exact reference-BVH walk redoes the ray
-                const float4 C = a.acc_tris[htri].c;
-                htri = (int32_t)__float_as_uint(C.y);
-                state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
-            }
-            int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
-            uint32_t fl = R.ld(CW_FLAGS);
-            Rng rng;
-            rng.d = R.ld(CW_RNG); rng.v0 = R.ld(CW_RNG + 1); rng.v1 = R.ld(CW_RNG + 2);
-            rng.v2 = R.ld(CW_RNG + 3); rng.v3 = R.ld(CW_RNG + 4); rng.v4 = R.ld(CW_RNG + 5);
-            C3 wgt = c3(R.ldd(CW_WGT), R.ldd(CW_WGT + 2), R.ldd(CW_WGT + 4));
-
-            // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
-            // a ray outside the Markstein preconditions, which takes the exact slow walk)
-            auto begin_trace = [&](V3 o, V3 d) -> bool {
-                wave_count(lcnt + 0, lane);
-                if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }   // spheres only
-                if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
-                if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
-                    htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
-                }
-                state = ST_TRACE;
-                return false;
-            };
-            // start sample n of pixel (px, py): camera ray, then memo or trace
-            auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
-                i = 0;
-                R.std_(CW_ACC, 0.0); R.std_(CW_ACC + 2, 0.0); R.std_(CW_ACC + 4, 0.0);
-                wgt = c3(1, 1, 1);
-                float u1 = 0.0f, u2 = 0.0f;
-                const bool lens = (fl & CF_LENS) != 0u;
-                if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
-                camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
-                wave_count(lcnt + 1, lane);
-                if (fl & CF_HAVE) {
-                    htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
-                    fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
-                    return true;
-                }
-                if (fl & CF_SHARE) {
-                    // the pixel's chunk 0 may have published the (sample-invariant) primary hit
-                    const uint32_t q = R.ld(CW_Q);
-                    const uint32_t tv = __hip_atomic_load(a.pmemo + 2 * (size_t)q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    if (tv != 0u) {
-                        htri = (int32_t)(tv - 2u);
-                        ht = __uint_as_float(a.pmemo[2 * (size_t)q + 1]);
-                        fl = (fl | CF_PRIMARY | CF_MEMO) & ~CF_SHARE;   // stores the unit memo on shading
-                        state = ST_SHADE;
-                        return true;
-                    }
-                }
-                fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
-                return begin_trace(ro, rd);
-            };
-
-            bool again = (state == ST_SHADE || state == ST_SLOW);
-            while (again) {
-                again = false;
-                if (state == ST_SLOW) {
-                    wave_count(lcnt + 3, lane);
-                    trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
-                               &htri, &ht);
-                }
-                state = ST_SHADE;
-                if (a.num_spheres && !(fl & CF_MEMO)) apply_spheres(a, ro, rd, &htri, &ht);
-                fl &= ~CF_MEMO;
-                if (fl & CF_PRIMARY) {
-                    fl = (fl | CF_HAVE) & ~CF_PRIMARY;
-                    R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
-                    if (fl & CF_OWNER) {
-                        const uint32_t q = R.ld(CW_Q);
-                        a.pmemo[2 * (size_t)q + 1] = __float_as_uint(ht);
-                        __hip_atomic_store(a.pmemo + 2 * (size_t)q, (uint32_t)(htri + 2), __ATOMIC_RELEASE,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                        fl &= ~CF_OWNER;
-                    }
-                }
-                // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
-                {
-                    int32_t tri = htri;
-                    float t = (float)((double)ht - 0.001);
-                    if ((double)t < 0.001) wgt = c3(0, 0, 0);
-                    if (t > kMaxFloat - 1) { wgt = c3(0, 0, 0); tri = 0; t = 0; }
-                    const V3 pos = ro + rd * t;
-                    const DMat* cm = a.mats + prim_mat(a, tri);
-                    const V3 normal = prim_normal(a, tri, pos);
-                    if (cm->emission[0] != 0) {
-                        C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
-                        acc = cadd(acc, cmul(wgt, mat_emission(cm)));
-                        R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
-                        wgt = c3(0, 0, 0);
-                    }
-                    V3 ldir;
-                    const float u = rng_uniform(rng);
-                    if (u < 0.5) {
-                        ldir = cosine_ray(normal, rng);
-                        wgt = cmul(wgt, cmulf(brdf(cm), (float)3.14159));
-                    } else {
-                        V3 p1;
-                        pick_light(a, rng, &p1);
-                        const V3 dd = p1 - pos;
-                        ldir = normalized(dd);
-                        const float cos_l = __builtin_fmaxf(0.0f, dot(ldir, normal));
-                        const float cos_o = __builtin_fmaxf(0.0f, dot(v3(0, -1, 0), ldir * -1));
-                        const float G = cos_l * cos_o / dot(dd, dd);
-                        wgt = cmul(wgt, cmulf(cmulf(brdf(cm), G), a.total_light_area));
-                        i = (i > D - 2) ? i : D - 2;
-                    }
-                    ro = pos;
-                    rd = ldir;
-                    ++i;
-                }
-                // advance to the next trace this lane needs
-                for (;;) {
-                    if (i >= D) {
-                        wave_count(lcnt + 2, lane);
-                        const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
-                        if (a.chunks == 1) {
-                            const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
-                            const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
-                            const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
-                            const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
-                            if (n >= a.spp) {
-                                float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
-                                o3[0] = (float)m0;
-                                o3[1] = (float)m1;
-                                o3[2] = (float)m2;
-                                state = ST_IDLE;
-                                break;
-                            }
-                            R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
-                        } else {
-                            // split pixel: keep L_n, finalize_pixels forms the ordered mean
-                            const size_t ch = (size_t)a.spp * a.npix;
-                            double* L = a.lbuf + (size_t)(n - 1) * a.npix + R.ld(CW_Q);
-                            L[0] = R.ldd(CW_ACC);
-                            L[ch] = R.ldd(CW_ACC + 2);
-                            L[2 * ch] = R.ldd(CW_ACC + 4);
-                            if ((uint32_t)n >= R.ld(CW_NEND)) {
-                                state = ST_IDLE;
-                                break;
-                            }
-                        }
-                        ++n;
-                        again = start_sample(px, py);
-                        break;
-                    }
-                    if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
-                        wave_count(lcnt + 1, lane);
-                        const float u = rng_uniform(rng);
-                        if (u < 0.5) { rng_next(rng); rng_next(rng); }
-                        else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
-                        ++i;
-                        continue;
-                    }
-                    wave_count(lcnt + 1, lane);
-                    again = begin_trace(ro, rd);
-                    break;
-                }
-            }
-
-            // refill: lanes whose pixel is finished take the next pixels of this shard
-            const uint64_t idle = __ballot(state == ST_IDLE);
-            if (idle) {
-                const uint32_t need = (uint32_t)__popcll(idle);
-                const int leader = __ffsll((long long)idle) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(a.pixel_counter, need);
-                base = __shfl(base, leader, 64);
-                if (state == ST_IDLE) {
-                    const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                    if (u >= a.nunits) {
-                        state = ST_DONE;
-                    } else {
-                        const uint32_t c = u / a.npix, q = u - c * a.npix;
-                        uint32_t px, py;
-                        if (unit_pixel(a, q, &px, &py)) {
-                            const uint32_t idx = morton2(px, py);
-                            // curand_init's state, computed for every unit by init_pixel_states
-                            rng.d = a.pix_states[5 * (size_t)a.nunits + u];
-                            rng.v0 = a.pix_states[u];
-                            rng.v1 = a.pix_states[(size_t)a.nunits + u];
-                            rng.v2 = a.pix_states[2 * (size_t)a.nunits + u];
-                            rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
-                            rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
-                            fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
-                            if (a.chunks > 1 && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
-                                fl |= (c == 0) ? CF_OWNER : CF_SHARE;
-                            n = (int)chunk_first(a, c) + 1;
-                            R.st(CW_PX, px); R.st(CW_PY, py);
-                            R.st(CW_NEND, chunk_first(a, c + 1));
-                            R.st(CW_Q, q);
-                            R.std_(CW_M, 0.0); R.std_(CW_M + 2, 0.0); R.std_(CW_M + 4, 0.0);
-                            start_sample(px, py);
-                        }
-                    }
-                }
-            }
-
-            R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i); R.st(CW_FLAGS, fl);
-            R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
-            R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
-            R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
-        }
+        if (state != ST_TRACE && state != ST_DONE) shade_lane(a, R, lane, state, ro, rd, htri, ht, w, S, lcnt);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
+    }
+    if (kCount) {
+        if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
+        const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
+        const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
+        if (lane == 0) {
+            atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
+            atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(a.counters + 0, lcnt[0]);
+        atomicAdd(a.counters + 1, lcnt[1]);
+        atomicAdd(a.counters + 4, lcnt[2]);
+        if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
+    }
+}
+
+// ------------------------------------------------------------------ path-pool kernel
+// The same state machine with kPaths > 64 paths per wave, so that a lane whose ray is done can
+// start another at once.  Each wave owns kPaths path records (ColdRec, CW_RO.. for the ray and
+// pending hit) and two LDS queues of path slots: TQ (ray ready to trace) and SQ (hit ready to
+// shade, or a path to refill).  Walk phase: lanes without a ray take the next TQ entry; a
+// finished walk stores the hit and queues the path on SQ; the phase ends when TQ is empty and
+// wf_threshold lanes are free (or nothing is tracing).  Shade phase: the free lanes shade SQ
+// paths, round after round, until SQ is empty, queueing each path's next ray on TQ.  Per path
+// the arithmetic and RNG draws are exactly those of render_unidir_wf (shade_lane is shared);
+// only which lane runs a path, and when, changes.
+// number of lanes below this one set in m (v_mbcnt)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+template <int kPaths>
+__device__ __forceinline__ ColdRec path_rec(const Args& a, uint32_t g)
+{
+    return ColdRec{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
+                   g * 4u, a.cold_stride * 4u};
+}
+
+template <bool kCount, int kMinWaves, int kPaths>
+__global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
+{
+    static_assert(kPaths >= 64 && kPaths <= 256 && (kPaths & (kPaths - 1)) == 0, "pool size: 64..256, power of 2");
+    extern __shared__ uint32_t lds_wf[];
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform (SGPR)
+    const int lane = threadIdx.x & 63;
+    // LDS: 4 waves' rings, then per wave TQ and SQ (kPaths u16 each), then the block counters.
+    // A TQ entry is slot | octant << 8: the ray's direction signs pick the near planes of the
+    // first node fetch before the ray itself arrives.
+    uint16_t* const TQ = reinterpret_cast<uint16_t*>(lds_wf + 4 * kWaveLdsWords) + wv * 2 * kPaths;
+    uint16_t* const SQ = TQ + kPaths;
+    unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords + 4 * kPaths);
+    if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
+    Counters cnt;
+    cnt.nodes = 0;
+    cnt.tris = 0;
+    cnt.leaf_steps = 0;
+    uint32_t walk_slots = 0, shade_slots = 0;
+    unsigned long long walk_clk = 0, shade_clk = 0;
+
+    Stack4 S;
+    S.ring = lds_wf + wv * kWaveLdsWords + lane;
+    S.stride = a.spill_stride;
+    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t path0 = (blockIdx.x * 4u + (uint32_t)wv) * (uint32_t)kPaths;
+
+    // every path starts idle, queued for shading (which gives it a unit)
+    for (int j = lane; j < kPaths; j += 64) {
+        SQ[j] = (uint16_t)j;
+        path_rec<kPaths>(a, path0 + (uint32_t)j).st(CW_PST, ST_IDLE);
+    }
+    __syncthreads();
+    // wave-uniform queue state (ring offsets mod kPaths)
+    uint32_t tq_head = 0, tq_n = 0, sq_head = 0, sq_n = kPaths;
+
+    uint32_t cur = kNone;   // path slot this lane is tracing
+    bool fresh = false;     // its ray is still to be fetched and set up (first step)
+    uint32_t state = ST_IDLE;
+    V3 ro = v3(0, 0, 0), rd = v3(0, 0, 1);
+    W4 w;
+    int32_t htri = -1;
+    float ht = kMaxFloat;
+
+    for (;;) {
+        // ---------------------------------------------------------------- walk
+        unsigned long long clk0 = 0;
+        if (kCount) clk0 = clock64();
+        for (;;) {
+            uint64_t idle = __ballot(cur == kNone);
+            if (tq_n > 0 && idle != 0ull) {
+                const uint32_t take = min((uint32_t)__popcll(idle), tq_n);
+                const uint32_t rank = lane_rank(idle);
+                if (cur == kNone && rank < take) {
+                    // the ray is fetched and set up inside the first step, with the root fetch in
+                    // flight (the root test passed when the ray was queued)
+                    const uint32_t e = TQ[(tq_head + rank) & (kPaths - 1)];
+                    cur = e & 255u;
+                    walk4_reset(w);
+                    w.nx = (e & 0x100u) ? 48u : 0u;   // == walk4_setup's choice (sign of d = sign of 1/d)
+                    w.ny = (e & 0x200u) ? 64u : 16u;
+                    w.nz = (e & 0x400u) ? 80u : 32u;
+                    fresh = true;
+                }
+                tq_head = (tq_head + take) & (kPaths - 1);
+                tq_n -= take;
+                idle = __ballot(cur == kNone);
+            }
+            if (idle == ~0ull) break;
+            if (tq_n == 0 && sq_n > 0 && (uint32_t)__popcll(idle) >= a.wf_threshold) break;
+            if (kCount) ++walk_slots;
+            bool fin = false;
+            if (cur != kNone) {
+                const auto setup = [&](W4& ww) {
+                    if (fresh) {
+                        const float4* pr = a.pray + 2 * (size_t)(path0 + cur);
+                        const float4 r0 = pr[0], r1 = pr[1];
+                        ro = v3(r0.x, r0.y, r0.z);
+                        rd = v3(r0.w, r1.x, r1.y);
+                        walk4_setup(ww, ro, rd);
+                        fresh = false;
+                    }
+                };
+                const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
+                                                     a.node_mask, cnt, setup);
+                if (!more) {
+                    // the winner's check against the reference BVH runs when the path is shaded
+                    float2* hp = reinterpret_cast<float2*>(a.pray + 2 * (size_t)(path0 + cur) + 1) + 1;
+                    *hp = make_float2(__uint_as_float(w.best_slot), w.best_t);
+                    path_rec<kPaths>(a, path0 + cur).st(CW_PST, (w.best_slot == kNone) ? ST_SHADE : ST_CHECK);
+                    fin = true;
+                }
+            }
+            const uint64_t done = __ballot(fin);
+            if (done) {
+                if (fin) {
+                    SQ[(sq_head + sq_n + lane_rank(done)) & (kPaths - 1)] = (uint16_t)cur;
+                    cur = kNone;
+                }
+                sq_n += (uint32_t)__popcll(done);
+            }
+        }
+        if (kCount) {
+            const unsigned long long c = clock64();
+            walk_clk += c - clk0;
+            clk0 = c;
+        }
+        if (sq_n == 0) break;   // nothing tracing, nothing queued: every path is done
+
+        // ---------------------------------------------------------------- shade rounds
+        for (bool first = true; sq_n > 0; first = false) {
+            const uint64_t avail = __ballot(cur == kNone);
+            if (avail == 0ull) break;   // (wf_threshold 0: every lane may still be tracing)
+            // only full rounds after the first: a remainder waits for the next shade phase
+            // (when nothing is tracing and nothing is queued to trace, it must go now)
+            if (!first && sq_n < (uint32_t)__popcll(avail) && (tq_n > 0 || avail != ~0ull)) break;
+            const uint32_t take = min((uint32_t)__popcll(avail), sq_n);
+            const uint32_t rank = lane_rank(avail);
+            uint32_t js = kNone;
+            if (cur == kNone && rank < take) js = SQ[(sq_head + rank) & (kPaths - 1)];
+            sq_head = (sq_head + take) & (kPaths - 1);
+            sq_n -= take;
+            if (kCount) ++shade_slots;
+            bool to_t = false, to_s = false;
+            if (js != kNone) {
+                const ColdRec P = path_rec<kPaths>(a, path0 + js);
+                float4* pr = a.pray + 2 * (size_t)(path0 + js);
+                state = P.ld(CW_PST);
+                {   // (garbage for a path that was never given a unit: shade_lane then only refills)
+                    const float4 r0 = pr[0], r1 = pr[1];
+                    ro = v3(r0.x, r0.y, r0.z);
+                    rd = v3(r0.w, r1.x, r1.y);
+                    htri = (int32_t)__float_as_uint(r1.z);
+                    ht = r1.w;
+                }
+                shade_lane(a, P, lane, state, ro, rd, htri, ht, w, S, lcnt);
+                if (state != ST_DONE) {
+                    // ST_TRACE: the next ray; otherwise shading is pending right after a refill
+                    // (memo hit, root miss, slow ray) and the hit travels with it
+                    pr[0] = make_float4(ro.x, ro.y, ro.z, rd.x);
+                    pr[1] = make_float4(rd.y, rd.z, __uint_as_float((uint32_t)htri), ht);
+                    if (state == ST_TRACE) {
+                        to_t = true;
+                    } else {
+                        P.st(CW_PST, state);
+                        to_s = true;
+                    }
+                }
+            }
+            const uint64_t bt = __ballot(to_t), bs = __ballot(to_s);
+            if (to_t) {
+                const uint32_t oct = (__float_as_uint(rd.x) >> 31) | ((__float_as_uint(rd.y) >> 31) << 1) |
+                                     ((__float_as_uint(rd.z) >> 31) << 2);
+                TQ[(tq_head + tq_n + lane_rank(bt)) & (kPaths - 1)] = (uint16_t)(js | (oct << 8));
+            }
+            if (to_s) SQ[(sq_head + sq_n + lane_rank(bs)) & (kPaths - 1)] = (uint16_t)js;
+            tq_n += (uint32_t)__popcll(bt);
+            sq_n += (uint32_t)__popcll(bs);
+        }
+        if (kCount) shade_clk += clock64() - clk0;
     }
     if (kCount) {
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
@@ -1128,6 +1354,9 @@ struct pt_ctx {
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
+    float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
+    size_t pray_words = 0;
+    int wf_pool = 0;                // paths per wave of the path-pool kernel (128 / 256), 0 = one per lane (PT_WF_POOL)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
@@ -1327,6 +1556,10 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_POOL")) {
+            const int v = atoi(e);
+            c->wf_pool = (v == 128 || v == 256) ? v : 0;
+        }
     }
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
     std::vector<DNode4> an;
@@ -1462,7 +1695,7 @@ void pt_destroy(pt_ctx* c)
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
-                    c->tone_thr, c->spheres};
+                    c->tone_thr, c->spheres, c->pray};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1546,7 +1779,9 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
         // one pixel's time): then each pixel is split into sample chunks.
         b.npix = a.ntiles_shard * 64u;
-        const uint64_t lanes = (uint64_t)blocks * 256u;
+        const uint32_t pool = (uint32_t)c->wf_pool;   // (pool kernels: 5 waves per SIMD)
+        const uint32_t paths_per_block = pool ? 4u * pool : 256u;
+        const uint64_t lanes = (uint64_t)blocks * paths_per_block;   // concurrently running paths
         uint32_t chunks = 1;
         if (c->wf_chunks > 0) chunks = (uint32_t)c->wf_chunks;
         else if (2 * (uint64_t)b.npix < 5 * lanes) chunks = (uint32_t)((24 * lanes + b.npix - 1) / b.npix);
@@ -1555,7 +1790,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         if ((uint64_t)b.npix * chunks > 0xffffffffull) chunks = 1;
         b.chunks = chunks;
         b.nunits = b.npix * chunks;
-        const uint32_t need = (b.nunits + 255) / 256;
+        const uint32_t need = (b.nunits + paths_per_block - 1) / paths_per_block;
         if (blocks > need) blocks = need;
         if (chunks > 1) {
             const size_t lw = (size_t)b.npix * (size_t)p->spp * 3;
@@ -1579,10 +1814,23 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             b.pmemo = c->pmemo;
         }
         const size_t per_lane = stack_words_per_lane(c);
-        if (int rc = ensure_spill(c, (per_lane + kColdWords) * (size_t)blocks * 256)) return rc;
+        if (int rc = ensure_spill(c, per_lane * (size_t)blocks * 256 + kColdWords * (size_t)blocks * paths_per_block))
+            return rc;
         b.spill = c->spill;
         b.spill_stride = blocks * 256;
+        b.cold_stride = blocks * paths_per_block;
         b.cold = c->spill + per_lane * (size_t)b.spill_stride;
+        if (pool) {
+            const size_t pw = (size_t)b.cold_stride * 8;   // 2 float4 per path
+            if (c->pray_words < pw) {
+                if (c->pray) (void)hipFree(c->pray);
+                c->pray = nullptr;
+                c->pray_words = 0;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pray), pw * 4));
+                c->pray_words = pw;
+            }
+            b.pray = c->pray;
+        }
         const size_t sw = (size_t)6 * b.nunits;
         if (c->pix_states_words < sw) {
             if (c->pix_states) (void)hipFree(c->pix_states);
@@ -1593,7 +1841,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         }
         b.pix_states = c->pix_states;
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
-        if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        const size_t lds_pool = (size_t)kWaveLdsWords * 4 * 4 + 4 * 4 * (size_t)pool + 4 * sizeof(unsigned long long);
+        if (pool == 128 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
+        else if (pool == 256 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 256>), dim3(blocks), dim3(256), lds_pool, stream, b);
+        else if (pool == 128) hipLaunchKernelGGL((render_unidir_pool<false, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
+        else if (pool == 256) hipLaunchKernelGGL((render_unidir_pool<false, 5, 256>), dim3(blocks), dim3(256), lds_pool, stream, b);
+        else if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);

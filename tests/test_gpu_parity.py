@@ -150,6 +150,34 @@ def test_sample_chunk_units_bit_exact(oracle_mod, monkeypatch, chunks, radius):
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("pool", ["128", "256"])
+@pytest.mark.parametrize("chunks,radius,flags,bounces", [
+    ("1", 0.0, 0, 3), ("3", 0.0, 0, 3), ("1", 0.05, pt.PT_FLAG_COUNT, 3),
+    ("5", 0.0, pt.PT_FLAG_NO_DEAD_PATH_SKIP | pt.PT_FLAG_NO_PRIMARY_CACHE, 8), ("1", 0.0, 0, 16)])
+def test_path_pool_kernel_bit_exact(oracle_mod, monkeypatch, pool, chunks, radius, flags, bounces):
+    """The path-pool kernel (kPaths paths per wave, LDS trace/shade queues; PT_WF_POOL): the same
+    image bits, sample count and reference trace count as the oracle, with whole-pixel and
+    sample-chunk units, the lens, the counting variant and both skip modes off."""
+    monkeypatch.setenv("PT_WF_POOL", pool)
+    monkeypatch.setenv("PT_WF_CHUNKS", chunks)
+    s = load_scene("cornell_blob")
+    w, h, spp = 40, 24, 5
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=bounces, flags=flags)
+        parts = np.zeros_like(img)
+        for k in range(2):
+            part, _ = r.render(cam, w, h, spp, bounces=bounces, flags=flags, shard_index=k, shard_count=2)
+            parts += part
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, bounces, 0, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert _bits_equal(parts, img.astype(np.float64)) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+    if flags & pt.PT_FLAG_COUNT:
+        assert st["node_tests"] > 0 and 0 < st["walk_lane_slots"]
+
+
 def test_rmse_and_properties_larger(oracle_mod, cb):
     """North-star tolerance on a subset of a larger render (oracle only on the subset)."""
     s, r = cb

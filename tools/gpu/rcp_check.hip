@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 __global__ void check(uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t* first)
 {
@@ -25,22 +26,23 @@ __global__ void check(uint32_t lo, uint32_t n, unsigned long long* bad, uint32_t
     }
 }
 
-int main()
+int main(int argc, char** argv)
 {
-    const uint32_t lo = 0x3727c5adu;   // T = 0x1.4f8b5ap-17
-    const uint32_t hi = 0x5f800000u;   // 2^64
+    // default: [T, 2^64]; `rcp_check LO HI` (hex float bits) checks another range
+    uint32_t lo = 0x3727c5adu;   // T = 0x1.4f8b5ap-17
+    uint32_t hi = 0x5f800000u;   // 2^64
+    if (argc == 3) { lo = (uint32_t)strtoul(argv[1], nullptr, 16); hi = (uint32_t)strtoul(argv[2], nullptr, 16); }
     const uint32_t n = hi - lo + 1u;
     unsigned long long* bad;
     uint32_t* first;
-    hipMalloc(&bad, 16);
-    hipMalloc(&first, 32);
-    hipMemset(bad, 0, 16);
-    hipMemset(first, 0, 32);
+    if (hipMalloc(&bad, 16) != hipSuccess || hipMalloc(&first, 32) != hipSuccess) return 2;
+    (void)hipMemset(bad, 0, 16);
+    (void)hipMemset(first, 0, 32);
     hipLaunchKernelGGL(check, dim3((n + 255) / 256), dim3(256), 0, 0, lo, n, bad, first);
     unsigned long long hb[2];
     uint32_t hf[8];
     if (hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost) != hipSuccess) { printf("hip error\n"); return 2; }
-    hipMemcpy(hf, first, 32, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hf, first, 32, hipMemcpyDeviceToHost);
     printf("checked %llu floats (both signs) in [0x%08x, 0x%08x]: %llu mismatches\n",
            2ull * n, lo, hi, hb[0]);
     for (int i = 0; i < 8 && i < (int)hb[0]; ++i) printf("  a bits 0x%08x\n", hf[i]);
