@@ -52,6 +52,7 @@ struct Args {
     uint32_t nunits;                // work units: npix * chunks
     uint32_t scene_fast;            // all scene coordinates admit the Markstein quotient
     uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
+    uint32_t wf_iters;              // shading iterations a lane may run per pass before yielding
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
@@ -666,12 +667,34 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 // samples until the lane needs a trace or its unit is done, then give finished lanes new units.
 // On return the lane's state is ST_TRACE (w set up for its ray), ST_SHADE / ST_SLOW (shading
 // pending: a memo hit, a root miss or a slow ray right after a refill) or ST_DONE.
+// Counting variant only: SEC(k) counts the waves that execute section k of the shading code
+// (counters[32 + k]; a profile of where shading issue slots go -- DESIGN.md "Measurement").
+enum : int { SEC_PASS = 0, SEC_CHECK, SEC_SLOW, SEC_BOUNCE, SEC_EMIT, SEC_COSINE, SEC_LIGHT, SEC_SAMPLE_END,
+             SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, kSections = 16 };
+#ifdef PT_SEC_MARKERS   // analysis builds: mark the sections in the ISA listing
+#define SEC_MARK(k) asm volatile("; SEC " #k)
+#else
+#define SEC_MARK(k)
+#endif
+#define SEC(k)                                                                                   \
+    do {                                                                                         \
+        SEC_MARK(k);                                                                             \
+        if (kCount) {                                                                            \
+            const uint64_t m_ = __ballot(1);                                                     \
+            if (lane == __ffsll((long long)m_) - 1)                                              \
+                atomicAdd(reinterpret_cast<uint32_t*>(lcnt + 4) + (k), 1u);                      \
+        }                                                                                        \
+    } while (0)
+
+template <bool kCount>
 __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
                                            int32_t& htri, float& ht, W4& w, const Stack4& S,
                                            unsigned long long* lcnt)
 {
     const int D = a.bounces;
+    SEC(SEC_PASS);
     if (state == ST_CHECK) {
+        SEC(SEC_CHECK);
         // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
         // (rare), the exact reference-BVH walk redoes the ray
         const float4 C = a.acc_tris[htri].c;
@@ -689,6 +712,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     // a ray outside the Markstein preconditions, which takes the exact slow walk)
     auto begin_trace = [&](V3 o, V3 d) -> bool {
         wave_count(lcnt + 0, lane);
+        SEC(SEC_BEGIN);
         if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }   // spheres only
         if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
         if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
@@ -705,7 +729,9 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         float u1 = 0.0f, u2 = 0.0f;
         const bool lens = (fl & CF_LENS) != 0u;
         if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
+        SEC(SEC_START);
         if (lens || !(fl & CF_CAMC)) {
+            SEC(SEC_CAMERA);
             camera_ray(a.cam, px, py, lens, u1, u2, &ro, &rd);
             if (!lens) {   // a pinhole ray is the same for every sample of the pixel
                 R.st(CW_CD, __float_as_uint(rd.x)); R.st(CW_CD + 1, __float_as_uint(rd.y)); R.st(CW_CD + 2, __float_as_uint(rd.z));
@@ -717,6 +743,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         }
         wave_count(lcnt + 1, lane);
         if (fl & CF_HAVE) {
+            SEC(SEC_MEMO);
             htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
             fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
             return true;
@@ -737,11 +764,17 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         return begin_trace(ro, rd);
     };
 
+    // A lane whose samples need no trace (primary memo hit on an emitter or a miss: the path is
+    // dead after bounce 0) would otherwise run sample after sample here while the rest of the
+    // wave waits; after wf_iters shading iterations it yields with its pending hit (ST_SHADE /
+    // ST_SLOW) and resumes in the next pass, alongside the other lanes' work.
     bool again = (state == ST_SHADE || state == ST_SLOW);
-    while (again) {
+    for (uint32_t iters = 0; again; ++iters) {
+        if (iters >= a.wf_iters) break;
         again = false;
         if (state == ST_SLOW) {
             wave_count(lcnt + 3, lane);
+            SEC(SEC_SLOW);
             trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
                        &htri, &ht);
         }
@@ -761,6 +794,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         }
         // bounce i of radianceAlongSingleStep2 (kernel.cu:427-512) on hit (htri, ht)
         {
+            SEC(SEC_BOUNCE);
             int32_t tri = htri;
             float t = (float)((double)ht - 0.001);
             if ((double)t < 0.001) wgt = c3(0, 0, 0);
@@ -769,6 +803,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             const DMat* cm = a.mats + prim_mat(a, tri);
             const V3 normal = prim_normal(a, tri, pos);
             if (cm->emission[0] != 0) {
+                SEC(SEC_EMIT);
                 C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
                 acc = cadd(acc, cmul(wgt, mat_emission(cm)));
                 R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
@@ -777,9 +812,11 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             V3 ldir;
             const float u = rng_uniform(rng);
             if (u < 0.5) {
+                SEC(SEC_COSINE);
                 ldir = cosine_ray(normal, rng);
                 wgt = cmul(wgt, cmulf(brdf(cm), (float)3.14159));
             } else {
+                SEC(SEC_LIGHT);
                 V3 p1;
                 pick_light(a, rng, &p1);
                 const V3 dd = p1 - pos;
@@ -798,6 +835,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         for (;;) {
             if (i >= D) {
                 wave_count(lcnt + 2, lane);
+                SEC(SEC_SAMPLE_END);
                 const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
                 if (a.chunks == 1) {
                     const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
@@ -831,6 +869,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             }
             if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
                 wave_count(lcnt + 1, lane);
+                SEC(SEC_DEAD);
                 const float u = rng_uniform(rng);
                 if (u < 0.5) { rng_next(rng); rng_next(rng); }
                 else { rng_next(rng); rng_next(rng); rng_next(rng); i = (i > D - 2) ? i : D - 2; }
@@ -846,6 +885,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     // refill: lanes whose pixel is finished take the next pixels of this shard
     const uint64_t idle = __ballot(state == ST_IDLE);
     if (idle) {
+        SEC(SEC_REFILL);
         const uint32_t need = (uint32_t)__popcll(idle);
         const int leader = __ffsll((long long)idle) - 1;
         uint32_t base = 0;
@@ -881,6 +921,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         }
     }
 
+    SEC(SEC_RECORD);
     R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i); R.st(CW_FLAGS, fl);
     R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
     R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
@@ -894,7 +935,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     // after the four waves' rings (kWaveLdsWords each): the block counters (traced, reference,
     // samples, slow walks)
     unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords);
-    if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
+    if (threadIdx.x < 4 + kSections / 2) lcnt[threadIdx.x] = 0ull;   // 4 counters + the section counts
     __syncthreads();
     const int lane = threadIdx.x & 63;
     Counters cnt;
@@ -948,7 +989,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // index, bounce, flags, RNG, path weight); accumulator, running mean, pixel and memo
         // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
-        if (state != ST_TRACE && state != ST_DONE) shade_lane(a, R, lane, state, ro, rd, htri, ht, w, S, lcnt);
+        if (state != ST_TRACE && state != ST_DONE) shade_lane<kCount>(a, R, lane, state, ro, rd, htri, ht, w, S, lcnt);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
@@ -967,6 +1008,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         atomicAdd(a.counters + 1, lcnt[1]);
         atomicAdd(a.counters + 4, lcnt[2]);
         if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
+    }
+    if (kCount && threadIdx.x < kSections) {
+        const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
+        if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
     }
 }
 
@@ -1005,7 +1050,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
     uint16_t* const TQ = reinterpret_cast<uint16_t*>(lds_wf + 4 * kWaveLdsWords) + wv * 2 * kPaths;
     uint16_t* const SQ = TQ + kPaths;
     unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords + 4 * kPaths);
-    if (threadIdx.x < 4) lcnt[threadIdx.x] = 0ull;
+    if (threadIdx.x < 4 + kSections / 2) lcnt[threadIdx.x] = 0ull;   // 4 counters + the section counts
     Counters cnt;
     cnt.nodes = 0;
     cnt.tris = 0;
@@ -1127,7 +1172,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
                     htri = (int32_t)__float_as_uint(r1.z);
                     ht = r1.w;
                 }
-                shade_lane(a, P, lane, state, ro, rd, htri, ht, w, S, lcnt);
+                shade_lane<kCount>(a, P, lane, state, ro, rd, htri, ht, w, S, lcnt);
                 if (state != ST_DONE) {
                     // ST_TRACE: the next ray; otherwise shading is pending right after a refill
                     // (memo hit, root miss, slow ray) and the hit travels with it
@@ -1168,6 +1213,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
         atomicAdd(a.counters + 1, lcnt[1]);
         atomicAdd(a.counters + 4, lcnt[2]);
         if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
+    }
+    if (kCount && threadIdx.x < kSections) {
+        const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
+        if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
     }
 }
 
@@ -1356,6 +1405,7 @@ struct pt_ctx {
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
     float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
     size_t pray_words = 0;
+    uint32_t wf_iters = 2;          // (PT_WF_ITERS)
     int wf_pool = 0;                // paths per wave of the path-pool kernel (128 / 256), 0 = one per lane (PT_WF_POOL)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
@@ -1556,6 +1606,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
         if (const char* e = getenv("PT_WF_POOL")) {
             const int v = atoi(e);
             c->wf_pool = (v == 128 || v == 256) ? v : 0;
@@ -1676,7 +1727,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         pt_destroy(c);
         return bail(rc);
     }
-    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 16 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 64 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), 16) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -1750,6 +1801,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.nunits = a.ntiles_shard * 64u;
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
+    a.wf_iters = c->wf_iters;
     a.node_mask = c->node_mask;
     a.nodes4 = c->nodes4;
     a.acc_tris = c->acc_tris;
@@ -1760,7 +1812,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const bool near_cam = cam_ext <= 64.0f * c->scene_extent;
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam;
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
     const uint32_t waves_per_cu = 16;
@@ -1773,7 +1825,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         Args b = a;
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
-        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long);
+        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + kSections * 4;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         // Work units: whole pixels, unless the shard has too few pixels to keep every resident
         // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
@@ -1841,7 +1893,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         }
         b.pix_states = c->pix_states;
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
-        const size_t lds_pool = (size_t)kWaveLdsWords * 4 * 4 + 4 * 4 * (size_t)pool + 4 * sizeof(unsigned long long);
+        const size_t lds_pool = (size_t)kWaveLdsWords * 4 * 4 + 4 * 4 * (size_t)pool + 4 * sizeof(unsigned long long) + kSections * 4;
         if (pool == 128 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
         else if (pool == 256 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 256>), dim3(blocks), dim3(256), lds_pool, stream, b);
         else if (pool == 128) hipLaunchKernelGGL((render_unidir_pool<false, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
@@ -1867,9 +1919,19 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev1, stream));
-    unsigned long long cnt[16];
+    unsigned long long cnt[64];
     HIP_TRY(hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    if (count) {
+        if (const char* path = getenv("PT_SECTION_DUMP")) {   // counting runs: shading section profile
+            if (FILE* f = fopen(path, "a")) {
+                fprintf(f, "sections");
+                for (int k = 0; k < kSections; ++k) fprintf(f, " %llu", cnt[32 + k]);
+                fprintf(f, "\n");
+                fclose(f);
+            }
+        }
+    }
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     if (st) {
