@@ -809,24 +809,74 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
                 wgt = c3(0, 0, 0);
             }
+            // The two sampling branches (kernel.cu:470-497 light sample, 498-509 cosine) with their
+            // common steps done once for the wave instead of once per branch: the draws (cosine:
+            // u1, u2; light: area pick, u, v -- the same first two positions), the one sin/cos
+            // (cosine theta, or a sphere light's phi), the normalisation and the f64 weight
+            // update.  Per lane the operations and their order are those of cosine_ray() /
+            // pick_light() + the reference's weight expressions.
             V3 ldir;
             const float u = rng_uniform(rng);
-            if (u < 0.5) {
-                SEC(SEC_COSINE);
-                ldir = cosine_ray(normal, rng);
-                wgt = cmul(wgt, cmulf(brdf(cm), (float)3.14159));
-            } else {
+            const bool cosb = u < 0.5;
+            const float r1 = rng_uniform(rng), r2 = rng_uniform(rng);
+            float r3 = 0.0f;
+            const DLight* L = nullptr;
+            bool need_sc = cosb;
+            float ang = r2;
+            if (!cosb) {
                 SEC(SEC_LIGHT);
+                r3 = rng_uniform(rng);
+                // area-CDF pick (pick_light); the scan stops once randArea <= 0
+                float ra = a.total_light_area * r1;
+                uint32_t sel = a.num_lights;
+                for (uint32_t j = 0; j < a.num_lights && ra > 0; ++j) {
+                    const float area = a.lights[j].area;
+                    if (ra < area && ra > 0) sel = j;
+                    ra -= area;
+                }
+                L = a.lights + sel;
+                if (L->pad != 0.0f) { need_sc = true; ang = r3; }   // sphere light: phi = 2*3.14159*v
+            } else {
+                SEC(SEC_COSINE);
+            }
+            float sn = 0.0f, cs = 0.0f;
+            if (need_sc) det_sincos((float)(2 * 3.14159 * (double)ang), &sn, &cs);
+            V3 vec;   // the direction before normalisation (light: dd = p1 - pos)
+            if (cosb) {
+                const float r = sqrtf(r1);
+                const float x = r * cs, z = r * sn;
+                const float y = sqrtf(__builtin_fmaxf(0.0f, 1.0f - r1));
+                const V3 tg = get_tangent(normal);
+                const V3 bt = cross(normal, tg);
+                vec = normal * y + tg * x + bt * z;
+            } else {
                 V3 p1;
-                pick_light(a, rng, &p1);
-                const V3 dd = p1 - pos;
-                ldir = normalized(dd);
+                if (L->pad != 0.0f) {
+                    const float zz = 1.0f - 2.0f * r2;
+                    const float rxy = sqrtf(__builtin_fmaxf(0.0f, 1.0f - zz * zz));
+                    p1 = v3(L->v0[0], L->v0[1], L->v0[2]) + v3(rxy * cs, rxy * sn, zz) * L->a1[0];
+                } else {
+                    float lu = r2, lv = r3;
+                    if ((double)(lu + lv) > 1.0) {
+                        lu = (float)((double)lu + 2 * (0.5 - (double)lu));
+                        lv = (float)((double)lv + 2 * (0.5 - (double)lv));
+                    }
+                    p1 = v3(L->v0[0], L->v0[1], L->v0[2]) + v3(L->a1[0], L->a1[1], L->a1[2]) * lu +
+                         v3(L->a2[0], L->a2[1], L->a2[2]) * lv;
+                }
+                vec = p1 - pos;
+            }
+            ldir = normalized(vec);
+            float f = (float)3.14159;
+            if (!cosb) {
                 const float cos_l = __builtin_fmaxf(0.0f, dot(ldir, normal));
                 const float cos_o = __builtin_fmaxf(0.0f, dot(v3(0, -1, 0), ldir * -1));
-                const float G = cos_l * cos_o / dot(dd, dd);
-                wgt = cmul(wgt, cmulf(cmulf(brdf(cm), G), a.total_light_area));
+                f = cos_l * cos_o / dot(vec, vec);   // G
                 i = (i > D - 2) ? i : D - 2;
             }
+            C3 bw = cmulf(brdf(cm), f);
+            if (!cosb) bw = cmulf(bw, a.total_light_area);
+            wgt = cmul(wgt, bw);
             ro = pos;
             rd = ldir;
             ++i;
