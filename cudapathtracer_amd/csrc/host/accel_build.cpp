@@ -52,7 +52,7 @@ struct Builder {
         }
     }
 
-    // 32-bin SAH split of items[b, e) (n > 1): partitions in place, returns the split point
+    // 128-bin SAH split of items[b, e) (n > 1): partitions in place, returns the split point
     size_t split(size_t b, size_t e) const
     {
         const size_t n = e - b;
@@ -64,7 +64,7 @@ struct Builder {
                 clo[k] = std::min(clo[k], tb[items[i]].c[k]);
                 chi[k] = std::max(chi[k], tb[items[i]].c[k]);
             }
-        constexpr int kBins = 32;
+        constexpr int kBins = 128;
         float best_cost = INFINITY;
         int best_axis = -1, best_split = 0;
         for (int k = 0; k < 3; ++k) {
