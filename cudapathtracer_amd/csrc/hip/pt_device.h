@@ -495,15 +495,29 @@ __device__ __forceinline__ f2 pk_fma(f2 a, float b, float c)
 {
     return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
 }
+// max/min of values known not to be NaN, as bare v_max3/v_min3 (IEEE mode would otherwise
+// canonicalize each operand the compiler cannot prove canonical, e.g. packed-FMA halves).
+__device__ __forceinline__ float entry4(float a, float b, float c, float cull_abs)
+{
+    float m, r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(r) : "s"(cull_abs), "v"(m));
+    return r;
+}
+__device__ __forceinline__ float exit4(float a, float b, float c, float limit)
+{
+    float m, r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+    asm("v_min_f32_e32 %0, %1, %2" : "=v"(r) : "v"(limit), "v"(m));
+    return r;
+}
 __device__ __forceinline__ void box_enter2(const W4& w, f2 nx, f2 ny, f2 nz, f2 fx, f2 fy, f2 fz, float limit,
-                                           float ncull, float& t0, float& t1)
+                                           float cull_abs, float& t0, float& t1)
 {
     const f2 ax = pk_fma(nx, w.inv.x, -w.oi.x), ay = pk_fma(ny, w.inv.y, -w.oi.y), az = pk_fma(nz, w.inv.z, -w.oi.z);
     const f2 bx = pk_fma(fx, w.inv.x, -w.oi.x), by = pk_fma(fy, w.inv.y, -w.oi.y), bz = pk_fma(fz, w.inv.z, -w.oi.z);
-    const float n0 = __builtin_fmaxf(__builtin_fmaxf(ax.x, ay.x), __builtin_fmaxf(az.x, ncull));
-    const float n1 = __builtin_fmaxf(__builtin_fmaxf(ax.y, ay.y), __builtin_fmaxf(az.y, ncull));
-    const float f0 = __builtin_fminf(__builtin_fminf(bx.x, by.x), __builtin_fminf(bz.x, limit));
-    const float f1 = __builtin_fminf(__builtin_fminf(bx.y, by.y), __builtin_fminf(bz.y, limit));
+    const float n0 = entry4(ax.x, ay.x, az.x, cull_abs), n1 = entry4(ax.y, ay.y, az.y, cull_abs);
+    const float f0 = exit4(bx.x, by.x, bz.x, limit), f1 = exit4(bx.y, by.y, bz.y, limit);
     t0 = (n0 <= f0) ? n0 : INFINITY;
     t1 = (n1 <= f1) ? n1 : INFINITY;
 }
@@ -521,13 +535,6 @@ __device__ __forceinline__ float4 ld_f4(const void* base, uint32_t off)
 __device__ __forceinline__ uint4 ld_u4(const void* base, uint32_t off)
 {
     return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + off);
-}
-
-__device__ __forceinline__ void cswap(float& ta, uint32_t& ra, float& tb, uint32_t& rb)
-{
-    const bool s = tb < ta;
-    const float t = s ? tb : ta; tb = s ? ta : tb; ta = t;
-    const uint32_t r = s ? rb : ra; rb = s ? ra : rb; ra = r;
 }
 
 // Per wave, LDS holds a node ring of kRing x 64 words followed by a leaf ring of kLeafRing x 64;
@@ -603,9 +610,9 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
         float t0, t1, t2, t3;
         box_enter2(w, f2{NX.x, NX.y}, f2{NY.x, NY.y}, f2{NZ.x, NZ.y}, f2{FX.x, FX.y}, f2{FY.x, FY.y}, f2{FZ.x, FZ.y},
-                   lim, -cull_abs, t0, t1);
+                   lim, cull_abs, t0, t1);
         box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
-                   lim, -cull_abs, t2, t3);
+                   lim, cull_abs, t2, t3);
         uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
         auto queue = [&](uint32_t slot) {
             if (w.leaf == kNone) { w.leaf = slot; return; }
@@ -616,16 +623,21 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         if ((r1 & kLeaf) && t1 != INFINITY) queue(r1 ^ kLeaf);
         if ((r2 & kLeaf) && t2 != INFINITY) queue(r2 ^ kLeaf);
         if ((r3 & kLeaf) && t3 != INFINITY) queue(r3 ^ kLeaf);
-        // inner children, nearest first; entries beyond the best are dropped
-        if (r0 & kLeaf) t0 = INFINITY;
-        if (r1 & kLeaf) t1 = INFINITY;
-        if (r2 & kLeaf) t2 = INFINITY;
-        if (r3 & kLeaf) t3 = INFINITY;
-        cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
-        if (t3 != INFINITY) push4(w, S, (__float_as_uint(t3) & ~node_mask) | r3);
-        if (t2 != INFINITY) push4(w, S, (__float_as_uint(t2) & ~node_mask) | r2);
-        if (t1 != INFINITY) push4(w, S, (__float_as_uint(t1) & ~node_mask) | r1);
-        w.node = (t0 != INFINITY) ? r0 : kNone;
+        // inner children, nearest first.  Each entered inner child becomes its stack entry
+        // (max(entry, 0) truncated to the bits above node_mask | node index): non-negative floats
+        // order like their bit patterns, so four u32 min/max pairs sort the entries by distance;
+        // leaves and boxes not entered become ~0 and sort last.
+        auto key = [&](float t, uint32_t r) -> uint32_t {
+            return ((r & kLeaf) || t == INFINITY) ? kNone
+                                                  : (((uint32_t)max((int32_t)__float_as_uint(t), 0) & ~node_mask) | r);
+        };
+        uint32_t k0 = key(t0, r0), k1 = key(t1, r1), k2 = key(t2, r2), k3 = key(t3, r3);
+        auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };
+        ksort(k0, k1); ksort(k2, k3); ksort(k0, k2); ksort(k1, k3); ksort(k1, k2);
+        if (k3 != kNone) push4(w, S, k3);
+        if (k2 != kNone) push4(w, S, k2);
+        if (k1 != kNone) push4(w, S, k1);
+        w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
     }
     if (w.leaf == kNone && w.lsp > 0) {
         --w.lsp;

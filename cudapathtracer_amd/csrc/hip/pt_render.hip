@@ -671,6 +671,7 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 // (counters[32 + k]; a profile of where shading issue slots go -- DESIGN.md "Measurement").
 enum : int { SEC_PASS = 0, SEC_CHECK, SEC_SLOW, SEC_BOUNCE, SEC_EMIT, SEC_COSINE, SEC_LIGHT, SEC_SAMPLE_END,
              SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, kSections = 16 };
+constexpr int kHist = 16;   // counting variant: walk steps per ray, log2 buckets (counters[48 + b])
 #ifdef PT_SEC_MARKERS   // analysis builds: mark the sections in the ISA listing
 #define SEC_MARK(k) asm volatile("; SEC " #k)
 #else
@@ -985,7 +986,9 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     // after the four waves' rings (kWaveLdsWords each): the block counters (traced, reference,
     // samples, slow walks)
     unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords);
-    if (threadIdx.x < 4 + kSections / 2) lcnt[threadIdx.x] = 0ull;   // 4 counters + the section counts
+    // 4 counters + the section counts + the walk-length histogram (counting variant)
+    if (threadIdx.x < 4 + kSections / 2 + kHist / 2) lcnt[threadIdx.x] = 0ull;
+    uint32_t* const lhist = reinterpret_cast<uint32_t*>(lcnt + 4) + kSections;
     __syncthreads();
     const int lane = threadIdx.x & 63;
     Counters cnt;
@@ -993,6 +996,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     cnt.tris = 0;
     cnt.leaf_steps = 0;
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
+    uint32_t trace_slots = 0, steps = 0;        // counting variant: lanes tracing per iteration; steps of this walk
     unsigned long long walk_clk = 0, shade_clk = 0;   // counting variant: wave-clock per phase
 
     // hot state: what the walk phase needs
@@ -1016,10 +1020,15 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
             if ((uint32_t)__popcll(__ballot(state != ST_TRACE && state != ST_DONE)) >= a.wf_threshold) break;
-            if (kCount) ++walk_slots;
+            if (kCount) { ++walk_slots; if (state == ST_TRACE) ++trace_slots; }
             if (state == ST_TRACE) {
                 const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
                                                      a.node_mask, cnt);
+                if (kCount) ++steps;
+                if (kCount && !more) {   // walk length histogram, log2 buckets
+                    atomicAdd(lhist + min(31 - __clz((int)steps), kHist - 1), 1u);
+                    steps = 0;
+                }
                 if (!more) {
                     // the winner's check against the reference BVH runs in the shading phase
                     htri = (int32_t)w.best_slot;
@@ -1047,9 +1056,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
+        const unsigned long long c11 = wave_sum(trace_slots);
         if (lane == 0) {
             atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
-            atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
+            atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7); atomicAdd(a.counters + 11, c11);
         }
     }
     __syncthreads();
@@ -1059,7 +1069,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         atomicAdd(a.counters + 4, lcnt[2]);
         if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
     }
-    if (kCount && threadIdx.x < kSections) {
+    if (kCount && threadIdx.x < kSections + kHist) {   // section counts, then the histogram
         const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
         if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
     }
@@ -1875,7 +1885,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         Args b = a;
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
-        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + kSections * 4;
+        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         // Work units: whole pixels, unless the shard has too few pixels to keep every resident
         // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
@@ -1977,7 +1987,9 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             if (FILE* f = fopen(path, "a")) {
                 fprintf(f, "sections");
                 for (int k = 0; k < kSections; ++k) fprintf(f, " %llu", cnt[32 + k]);
-                fprintf(f, "\n");
+                fprintf(f, "\nwalk_hist");
+                for (int k = 0; k < kHist; ++k) fprintf(f, " %llu", cnt[32 + kSections + k]);
+                fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu\n", cnt[11], cnt[5], cnt[2], cnt[6]);
                 fclose(f);
             }
         }
