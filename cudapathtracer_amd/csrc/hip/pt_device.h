@@ -319,6 +319,11 @@ __device__ __forceinline__ void pin(uint4& v)
 {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
+// The same for a value that is only read afterwards: an input-only use (no register copies).
+__device__ __forceinline__ void pin_use(const float4& v)
+{
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+}
 
 // The smallest float whose double is >= 0.00001: for float a, (double)a < 0.00001 <=> a < kTriEps.
 constexpr float kTriEps = 0x1.4f8b5ap-17f;
@@ -539,17 +544,26 @@ __device__ __forceinline__ uint4 ld_u4(const void* base, uint32_t off)
 
 // Per wave, LDS holds a node ring of kRing x 64 words followed by a leaf ring of kLeafRing x 64;
 // `ring` points at this lane's word 0 (wave base + lane).
+// The lane's HBM spill column (entry k >= kRing at spill()[(k - kRing) * stride]) is addressed from
+// a byte offset the kernel keeps in a register anyway (its shading record's lane offset), masked,
+// so the walk holds no 64-bit spill pointer.
 struct Stack4 {
-    uint32_t* ring;       // LDS: node entry k at ring[(k % kRing) * 64], queued leaf k at ring[(kRing + k) * 64]
-    uint32_t* spill;      // HBM: node entry k >= kRing at spill[(k - kRing) * stride]
+    uint32_t* ring;            // LDS: node entry k at ring[(k % kRing) * 64], queued leaf k at ring[(kRing + k) * 64]
+    uint32_t* spill_base;      // HBM (uniform)
+    const uint32_t* lane_off;  // -> lane byte offset (a caller variable), & off_mask
+    uint32_t off_mask;
     uint32_t stride;
+    __device__ __forceinline__ uint32_t* spill() const
+    {
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spill_base) + (*lane_off & off_mask));
+    }
 };
 constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
 
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 {
     const int slot = (w.sp & (kRing - 1)) * 64;   // sp >= 0, kRing a power of two
-    if (w.sp >= kRing) S.spill[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
+    if (w.sp >= kRing) S.spill()[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
     S.ring[slot] = e;
     ++w.sp;
 }
@@ -559,7 +573,7 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
     --w.sp;
     const int slot = (w.sp & (kRing - 1)) * 64;
     const uint32_t e = S.ring[slot];
-    if (w.sp >= kRing) S.ring[slot] = S.spill[(size_t)(w.sp - kRing) * S.stride];
+    if (w.sp >= kRing) S.ring[slot] = S.spill()[(size_t)(w.sp - kRing) * S.stride];
     return e;
 }
 
@@ -592,7 +606,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const float4 NZ = ld_f4(nodes, oz), FZ = ld_f4(nodes, oz ^ 112u);
     uint4 ch = ld_u4(nodes, nb + 96u);
     setup(w);
-    pin(A); pin(B); pin(C);   // (the node's fields feed unconditional tests: no pin needed)
+    pin_use(A); pin_use(B); pin_use(C);   // (the node's fields feed unconditional tests: no pin needed)
     if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
         const float t = tri_hit_rec<true>(o, d, A, B, C);
@@ -634,9 +648,21 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         uint32_t k0 = key(t0, r0), k1 = key(t1, r1), k2 = key(t2, r2), k3 = key(t3, r3);
         auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };
         ksort(k0, k1); ksort(k2, k3); ksort(k0, k2); ksort(k1, k3); ksort(k1, k2);
-        if (k3 != kNone) push4(w, S, k3);
-        if (k2 != kNone) push4(w, S, k2);
-        if (k1 != kNone) push4(w, S, k1);
+        if (__ballot(w.sp > kRing - 3) == 0ull) {
+            // no ring wrap-around possible in this wave: the valid keys (a sorted prefix) go to
+            // slots sp.. far-to-near with three unconditional writes (the slots above the new top
+            // are free)
+            const bool v1 = k1 != kNone, v2 = k2 != kNone, v3 = k3 != kNone;
+            uint32_t* const top = S.ring + w.sp * 64;
+            top[0] = v3 ? k3 : (v2 ? k2 : k1);
+            top[64] = v3 ? k2 : k1;
+            top[128] = k1;
+            w.sp += (int)v1 + (int)v2 + (int)v3;
+        } else {
+            if (k3 != kNone) push4(w, S, k3);
+            if (k2 != kNone) push4(w, S, k2);
+            if (k1 != kNone) push4(w, S, k1);
+        }
         w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
     }
     if (w.leaf == kNone && w.lsp > 0) {

@@ -776,7 +776,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         if (state == ST_SLOW) {
             wave_count(lcnt + 3, lane);
             SEC(SEC_SLOW);
-            trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
+            trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs,
                        &htri, &ht);
         }
         state = ST_SHADE;
@@ -997,29 +997,36 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     cnt.leaf_steps = 0;
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
     uint32_t trace_slots = 0, steps = 0;        // counting variant: lanes tracing per iteration; steps of this walk
+    uint32_t start_wait = 0;                    // counting variant: lanes without a ray when a walk phase starts
     unsigned long long walk_clk = 0, shade_clk = 0;   // counting variant: wave-clock per phase
 
     // hot state: what the walk phase needs
     uint32_t state = ST_IDLE;
     V3 ro = v3(0, 0, 0), rd = v3(0, 0, 1);
     W4 w;
-    int32_t htri = -1;
-    float ht = kMaxFloat;
+    int32_t& htri = reinterpret_cast<int32_t&>(w.best_slot);   // the pending hit lives in the walk state
+    float& ht = w.best_t;                                        // (a finished walk leaves it there)
+    htri = -1;
+    ht = kMaxFloat;
     Stack4 S;
     S.ring = lds_wf + (threadIdx.x >> 6) * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
-    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
                     (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.cold_stride * 4u};
+    S.spill_base = a.spill;   // spill column of lane g at byte offset 4g: R.voff
+    S.lane_off = &R.voff;
+    S.off_mask = ~0u;
 
     for (;;) {
         // ---------------------------------------------------------------- walk
         unsigned long long clk0 = 0;
         if (kCount) clk0 = clock64();
+        const uint64_t live = __ballot(state != ST_DONE);   // (no lane becomes DONE while walking)
+        if (kCount) start_wait += (uint32_t)__popcll(live & ~__ballot(state == ST_TRACE));
         for (;;) {
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
-            if ((uint32_t)__popcll(__ballot(state != ST_TRACE && state != ST_DONE)) >= a.wf_threshold) break;
+            if ((uint32_t)__popcll(live & ~tracing) >= a.wf_threshold) break;   // lanes waiting to shade
             if (kCount) { ++walk_slots; if (state == ST_TRACE) ++trace_slots; }
             if (state == ST_TRACE) {
                 const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
@@ -1031,8 +1038,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 }
                 if (!more) {
                     // the winner's check against the reference BVH runs in the shading phase
-                    htri = (int32_t)w.best_slot;
-                    ht = w.best_t;
+                    // (htri, ht) == (w.best_slot, w.best_t): the hit is already in place
                     state = (w.best_slot == kNone) ? ST_SHADE : ST_CHECK;
                 }
             }
@@ -1060,6 +1066,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (lane == 0) {
             atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
             atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7); atomicAdd(a.counters + 11, c11);
+            atomicAdd(a.counters + 12, (unsigned long long)start_wait);
         }
     }
     __syncthreads();
@@ -1121,7 +1128,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
     Stack4 S;
     S.ring = lds_wf + wv * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
-    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane_off = (blockIdx.x * blockDim.x + threadIdx.x) * 4u;
+    S.spill_base = a.spill;
+    S.lane_off = &lane_off;
+    S.off_mask = ~0u;
     const uint32_t path0 = (blockIdx.x * 4u + (uint32_t)wv) * (uint32_t)kPaths;
 
     // every path starts idle, queued for shading (which gives it a unit)
@@ -1326,7 +1336,10 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
     uint32_t* const wave_lds = lds_tr + (threadIdx.x >> 6) * a.stack_words;
     S.ring = wave_lds + lane;
     S.stride = a.spill_stride;
-    S.spill = a.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane_off = (blockIdx.x * blockDim.x + threadIdx.x) * 4u;
+    S.spill_base = a.spill;
+    S.lane_off = &lane_off;
+    S.off_mask = ~0u;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
         const V3 o = v3(rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]);
         const V3 d = v3(rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]);
@@ -1338,7 +1351,7 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
             const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
             htri = h.tri; ht = h.t;
         } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
-            trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs, &htri, &ht);
+            trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs, &htri, &ht);
         } else {
             W4 w;
             if (walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
@@ -1353,7 +1366,7 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
                 }
                 if (!ok) {
                     atomicAdd(a.counters + 8, 1ull);
-                    trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill, S.stride, a.cull_rel, a.cull_abs,
+                    trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs,
                                &htri, &ht);
                 }
             }
@@ -1989,7 +2002,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 for (int k = 0; k < kSections; ++k) fprintf(f, " %llu", cnt[32 + k]);
                 fprintf(f, "\nwalk_hist");
                 for (int k = 0; k < kHist; ++k) fprintf(f, " %llu", cnt[32 + kSections + k]);
-                fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu\n", cnt[11], cnt[5], cnt[2], cnt[6]);
+                fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu start_wait %llu\n", cnt[11], cnt[5],
+                        cnt[2], cnt[6], cnt[12]);
                 fclose(f);
             }
         }
