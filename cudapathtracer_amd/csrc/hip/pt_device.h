@@ -247,6 +247,7 @@ struct Counters {
     uint32_t nodes;        // node records fetched (64 B culled walk, 32 B reference walk)
     uint32_t tris;         // triangle records tested (48 B)
     uint32_t leaf_steps;   // walk steps that tested at least one triangle
+    uint32_t top = 0;      // BVH4 node visits served by the LDS copy of the tree's top
 };
 
 // ------------------------------------------------------------------ exact division, cheaply
@@ -324,6 +325,10 @@ __device__ __forceinline__ void pin_use(const float4& v)
 {
     asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
 }
+__device__ __forceinline__ void pin_use1(float v)
+{
+    asm volatile("" ::"v"(v));
+}
 
 // The smallest float whose double is >= 0.00001: for float a, (double)a < 0.00001 <=> a < kTriEps.
 constexpr float kTriEps = 0x1.4f8b5ap-17f;
@@ -351,31 +356,77 @@ __device__ __forceinline__ float div_mk_nz(float x, float d, float y)
     return __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
 }
 
-// triIntersect (modelLoader.h:49-83) on a record already in registers; kMk: RN(1/a) and
-// Markstein quotients.
-template <bool kMk>
-__device__ __forceinline__ float tri_hit_rec(V3 o, V3 d, float4 A, float4 B, float4 C)
+// Packed f32 pairs (VOP3P): one v_pk_* instruction performs two independent IEEE f32 operations,
+// each bit-identical to the scalar instruction (same rounding, same denormal mode; no
+// contraction).  op_sel / op_sel_hi pick, per result half, the lo or hi word of each source
+// (so swizzles and broadcasts are free); neg_lo / neg_hi negate a source for that half
+// (a + (-b) is IEEE a - b, and (-a) + b is b - a).
+typedef float f2 __attribute__((ext_vector_type(2)));
+#define PK2(op, mods, a, b)                                                                   \
+    ({                                                                                        \
+        f2 r_;                                                                                \
+        asm("v_pk_" op "_f32 %0, %1, %2 " mods : "=v"(r_) : "v"(a), "v"(b));                  \
+        r_;                                                                                   \
+    })
+#define PK3(op, mods, a, b, c)                                                                \
+    ({                                                                                        \
+        f2 r_;                                                                                \
+        asm("v_pk_" op "_f32 %0, %1, %2, %3 " mods : "=v"(r_) : "v"(a), "v"(b), "v"(c));      \
+        r_;                                                                                   \
+    })
+__device__ __forceinline__ f2 bcast(float x)   // x in the lo word (the hi word is never read)
 {
-    const V3 v0 = v3(A.x, A.y, A.z), e1 = v3(A.w, B.x, B.y), e2 = v3(B.z, B.w, C.x);
-    const V3 q = cross(d, e2);
-    const float a = dot(e1, q);
+    f2 r;
+    r.x = x;
+    return r;
+}
+
+// Render-path triangle record (acc_tris) in registers: the words are permuted so that the
+// operand pairs of the packed test sit in aligned register pairs:
+//   A = {v0.x, v0.y, e1.x, e1.y}, B = {e2.x, e2.y, v0.z, e1.z}, C = {e2.z, id, rank, parent};
+// the test reads A, B and e2.z only (36 B: vector-memory data return is paid per byte of the whole
+// wave-instruction, so the third load is a single dword).
+// triIntersect (modelLoader.h:49-83) with RN(1/a) and Markstein quotients, the x/y halves of every
+// vector expression as one packed op: per component the same IEEE operations in the same order
+// as tri_hit<true> (dot = (x*x' + y*y') + z*z'; cross component = product - product), i.e. the
+// same bits.  O, DD = {o.x, o.y}, {d.x, d.y}.
+__device__ __forceinline__ float tri_hit_pk(f2 O, float oz, f2 DD, float dz, float4 A, float4 B, float e2z)
+{
+    const f2 V0 = {A.x, A.y}, E1 = {A.z, A.w}, E2 = {B.x, B.y}, VZ = {B.z, B.w}, CZ = bcast(e2z);
+    const float v0z = B.z, e1z = B.w;
+    // q = cross(d, e2)
+    const f2 P1 = PK2("mul", "op_sel:[1,0] op_sel_hi:[0,0]", DD, CZ);          // {dy*e2z, dx*e2z}
+    const f2 P2 = PK2("mul", "op_sel:[0,1] op_sel_hi:[0,0]", bcast(dz), E2);   // {dz*e2y, dz*e2x}
+    const f2 Q = PK2("add", "neg_lo:[0,1] neg_hi:[1,0]", P1, P2);              // {qx, qy}
+    const f2 P3 = PK2("mul", "op_sel:[0,1] op_sel_hi:[1,0]", DD, E2);          // {dx*e2y, dy*e2x}
+    const float qz = P3.x - P3.y;
+    const f2 EQ = PK2("mul", "", E1, Q);
+    const float a = (EQ.x + EQ.y) + e1z * qz;                                   // dot(e1, q)
     if (__builtin_fabsf(a) < kTriEps) return kMaxFloat;   // == (double)|a| < 0.00001, NaN included
-    const V3 w = o - v0;
-    V3 s;
-    if (kMk) {
-        const float ya = rcp_rn(a);
-        s = v3(div_mk_nz(w.x, a, ya), div_mk_nz(w.y, a, ya), div_mk_nz(w.z, a, ya));
-    } else {
-        s = w / a;
-    }
-    const V3 r = cross(s, e1);
-    const float b0 = dot(s, q);
-    const float b1 = dot(r, d);
+    // s = (o - v0) / a
+    const f2 W = PK2("add", "neg_lo:[0,1] neg_hi:[0,1]", O, V0);
+    const float wz = oz - v0z;
+    const float ya = rcp_rn(a);
+    const f2 Q0 = PK2("mul", "op_sel_hi:[1,0]", W, bcast(ya));
+    const f2 RR = PK3("fma", "op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]", Q0, bcast(a), W);
+    const f2 S = PK3("fma", "op_sel_hi:[1,0,1]", RR, bcast(ya), Q0);           // div_mk_nz(w.xy, a, ya)
+    const float sz = div_mk_nz(wz, a, ya);
+    // r = cross(s, e1)
+    const f2 R1 = PK2("mul", "op_sel:[1,1] op_sel_hi:[0,1]", S, VZ);           // {sy*e1z, sx*e1z}
+    const f2 R2 = PK2("mul", "op_sel:[0,1] op_sel_hi:[0,0]", bcast(sz), E1);   // {sz*e1y, sz*e1x}
+    const f2 R = PK2("add", "neg_lo:[0,1] neg_hi:[1,0]", R1, R2);              // {rx, ry}
+    const f2 R3 = PK2("mul", "op_sel:[0,1] op_sel_hi:[1,0]", S, E1);           // {sx*e1y, sy*e1x}
+    const float rz = R3.x - R3.y;
+    const f2 SQ = PK2("mul", "", S, Q);
+    const float b0 = (SQ.x + SQ.y) + sz * qz;                                   // dot(s, q)
+    const f2 RD = PK2("mul", "", R, DD);
+    const float b1 = (RD.x + RD.y) + rz * dz;                                   // dot(r, d)
     const float b2 = 1.0f - b0 - b1;
     if (b0 < 0.0f) return kMaxFloat;
     if (b1 < 0.0f) return kMaxFloat;
     if (b2 < 0.0f) return kMaxFloat;
-    return dot(e2, r);
+    const f2 ER = PK2("mul", "", E2, R);
+    return (ER.x + ER.y) + e2z * rz;                                            // dot(e2, r)
 }
 
 // triIntersect (modelLoader.h:49-83); kMk: one IEEE reciprocal of `a`, Markstein quotients.
@@ -495,7 +546,6 @@ __device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root
 // far ones, and no NaN can arise (finite bounds, |inv| <= 2^100).  Returns max(entry, -cull_abs)
 // (+inf = not entered): the box is entered iff max(entry, -cull_abs) <= min(exit, limit), which is
 // entry <= exit && exit >= -cull_abs && entry <= limit.  Entries below -cull_abs only sort first.
-typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, float b, float c)
 {
     return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
@@ -541,6 +591,30 @@ __device__ __forceinline__ uint4 ld_u4(const void* base, uint32_t off)
 {
     return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + off);
 }
+// The same with the address space explicit (LDS: ds_read_b128; global: global_load_dwordx4), so
+// that the two sides of a branch can never be merged into one flat load.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 lds_f4(const char* base, uint32_t off)
+{
+    const f4v v = *(__attribute__((address_space(3))) const f4v*)(base + off);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 lds_u4(const char* base, uint32_t off)
+{
+    const u4v v = *(__attribute__((address_space(3))) const u4v*)(base + off);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 glb_f4(const void* base, uint32_t off)
+{
+    const f4v v = *(__attribute__((address_space(1))) const f4v*)(reinterpret_cast<const char*>(base) + off);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 glb_u4(const void* base, uint32_t off)
+{
+    const u4v v = *(__attribute__((address_space(1))) const u4v*)(reinterpret_cast<const char*>(base) + off);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Per wave, LDS holds a node ring of kRing x 64 words followed by a leaf ring of kLeafRing x 64;
 // `ring` points at this lane's word 0 (wave base + lane).
@@ -553,12 +627,20 @@ struct Stack4 {
     const uint32_t* lane_off;  // -> lane byte offset (a caller variable), & off_mask
     uint32_t off_mask;
     uint32_t stride;
+    const char* top = nullptr;   // LDS copy of BVH4 nodes 0..ntop-1 (kTopNodeBytes each), or none
+    uint32_t ntop = 0;
     __device__ __forceinline__ uint32_t* spill() const
     {
         return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spill_base) + (*lane_off & off_mask));
     }
 };
 constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
+// BVH4 nodes 0..top-1 (the best-first top of the tree, pt_create) are staged in the block's LDS
+// by the wavefront kernel, 112 B each (the node without its pad; stride 28 dwords, so 16
+// consecutive nodes occupy disjoint banks): lanes visiting them read LDS instead of issuing
+// vector-memory loads -- the kernel's limiting pipe (TA/TD, DESIGN.md "Measurement").
+constexpr uint32_t kTopNodeBytes = 112;
+constexpr uint32_t kTopNodesMax = 64;   // what fits next to the rings with 5 blocks of 256 threads per CU (66 does not)
 
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 {
@@ -598,23 +680,41 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const bool leaf = w.leaf != kNone;
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
     const uint32_t tb = mul48(leaf ? w.leaf : 0u);
-    float4 A = ld_f4(tris, tb), B = ld_f4(tris, tb + 16u), C = ld_f4(tris, tb + 32u);
-    const uint32_t nb = (visit ? w.node : 0u) * 128u;
-    const uint32_t ox = nb | w.nx, oy = nb | w.ny, oz = nb | w.nz;
-    const float4 NX = ld_f4(nodes, ox), FX = ld_f4(nodes, ox ^ 48u);
-    const float4 NY = ld_f4(nodes, oy), FY = ld_f4(nodes, oy ^ 80u);
-    const float4 NZ = ld_f4(nodes, oz), FZ = ld_f4(nodes, oz ^ 112u);
-    uint4 ch = ld_u4(nodes, nb + 96u);
+    float4 A = ld_f4(tris, tb), B = ld_f4(tris, tb + 16u);
+    float e2z = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tris) + tb + 32u);
+    // a lane with no node to visit reads node 0 (the LDS copy when there is one)
+    const uint32_t nidx = visit ? w.node : 0u;
+    float4 NX, FX, NY, FY, NZ, FZ;
+    uint4 ch;
+    // Every lane reads the LDS copy first (a deep node's lane reads node 0: a broadcast), then the
+    // deep nodes' lanes overwrite it with their global loads -- in this order, because the loads
+    // write the same registers and an LDS read issued behind outstanding global loads to them
+    // would have to wait out their whole latency.
+    if (S.ntop != 0u) {
+        const char* const lb = S.top + (nidx < S.ntop ? nidx : 0u) * kTopNodeBytes;
+        NX = lds_f4(lb, w.nx); FX = lds_f4(lb, w.nx ^ 48u);
+        NY = lds_f4(lb, w.ny); FY = lds_f4(lb, w.ny ^ 80u);
+        NZ = lds_f4(lb, w.nz); FZ = lds_f4(lb, w.nz ^ 112u);
+        ch = lds_u4(lb, 96u);
+    }
+    if (nidx >= S.ntop) {
+        const uint32_t nb = nidx * 128u;
+        const uint32_t ox = nb | w.nx, oy = nb | w.ny, oz = nb | w.nz;
+        NX = glb_f4(nodes, ox); FX = glb_f4(nodes, ox ^ 48u);
+        NY = glb_f4(nodes, oy); FY = glb_f4(nodes, oy ^ 80u);
+        NZ = glb_f4(nodes, oz); FZ = glb_f4(nodes, oz ^ 112u);
+        ch = glb_u4(nodes, nb + 96u);
+    }
     setup(w);
-    pin_use(A); pin_use(B); pin_use(C);   // (the node's fields feed unconditional tests: no pin needed)
-    if (kCount) { if (visit) ++cnt.nodes; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
+    pin_use(A); pin_use(B); pin_use1(e2z);   // (the node's fields feed unconditional tests: no pin needed)
+    if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
-        const float t = tri_hit_rec<true>(o, d, A, B, C);
+        const float t = tri_hit_pk(f2{o.x, o.y}, o.z, f2{d.x, d.y}, d.z, A, B, e2z);
         // ties go to the lower reference DFS rank (the reference's first-visited); exact ties are
-        // rare, so the best's rank is re-read rather than kept in a register
+        // rare, so both ranks are read only then
         if (0.0f < t && (t < w.best_t ||
                          (t == w.best_t && w.best_slot != kNone &&
-                          __float_as_uint(C.z) < __float_as_uint(tris[w.best_slot].c.z)))) {
+                          __float_as_uint(tris[w.leaf].c.z) < __float_as_uint(tris[w.best_slot].c.z)))) {
             w.best_t = t; w.best_slot = w.leaf;
         }
         w.leaf = kNone;

@@ -7,6 +7,7 @@
 // tiles from an atomic counter; tile t belongs to shard t % shard_count.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -54,6 +55,7 @@ struct Args {
     uint32_t wf_threshold;          // leave the walk when this many lanes wait for shading
     uint32_t wf_iters;              // shading iterations a lane may run per pass before yielding
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
+    uint32_t top_nodes;             // wavefront kernel: BVH4 nodes 0..top_nodes-1 staged in LDS
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
@@ -998,6 +1000,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
     uint32_t trace_slots = 0, steps = 0;        // counting variant: lanes tracing per iteration; steps of this walk
     uint32_t start_wait = 0;                    // counting variant: lanes without a ray when a walk phase starts
+    uint32_t itc[6] = {0, 0, 0, 0, 0, 0};       // counting variant: walk-iteration classes (counters[14..19])
     unsigned long long walk_clk = 0, shade_clk = 0;   // counting variant: wave-clock per phase
 
     // hot state: what the walk phase needs
@@ -1016,6 +1019,15 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.spill_base = a.spill;   // spill column of lane g at byte offset 4g: R.voff
     S.lane_off = &R.voff;
     S.off_mask = ~0u;
+    // the top of the BVH4 in LDS (after the rings and counters; kTopNodeBytes per node)
+    float4* const ltop = reinterpret_cast<float4*>(lcnt + 4 + (kSections + kHist) / 2);
+    for (uint32_t k = threadIdx.x; k < a.top_nodes * (kTopNodeBytes / 16); k += blockDim.x) {
+        const uint32_t nd = k / (kTopNodeBytes / 16), q = k - nd * (kTopNodeBytes / 16);
+        ltop[k] = reinterpret_cast<const float4*>(a.nodes4 + nd)[q];
+    }
+    S.top = reinterpret_cast<const char*>(ltop);
+    S.ntop = a.top_nodes;
+    __syncthreads();
 
     for (;;) {
         // ---------------------------------------------------------------- walk
@@ -1027,7 +1039,18 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
             if ((uint32_t)__popcll(live & ~tracing) >= a.wf_threshold) break;   // lanes waiting to shade
-            if (kCount) { ++walk_slots; if (state == ST_TRACE) ++trace_slots; }
+            if (kCount) {
+                ++walk_slots;
+                if (state == ST_TRACE) ++trace_slots;
+                // wave iterations by the number of lanes needing a global node fetch (0, 1-4, 5-8,
+                // more), with no pending leaf in the wave, and with neither
+                const bool vis = state == ST_TRACE && w.node != kNone && w.lsp <= kLeafRing - 4;
+                const uint32_t deep = (uint32_t)__popcll(__ballot(vis && w.node >= S.ntop));
+                const bool noleaf = __ballot(state == ST_TRACE && w.leaf != kNone) == 0ull;
+                ++itc[deep == 0u ? 0 : deep <= 4u ? 1 : deep <= 8u ? 2 : 3];
+                if (noleaf) ++itc[4];
+                if (noleaf && deep == 0u) ++itc[5];
+            }
             if (state == ST_TRACE) {
                 const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
                                                      a.node_mask, cnt);
@@ -1061,12 +1084,15 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     if (kCount) {
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
+        const unsigned long long c13 = wave_sum(cnt.top);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
         const unsigned long long c11 = wave_sum(trace_slots);
         if (lane == 0) {
             atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
             atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7); atomicAdd(a.counters + 11, c11);
             atomicAdd(a.counters + 12, (unsigned long long)start_wait);
+            atomicAdd(a.counters + 13, c13);
+            for (int k = 0; k < 6; ++k) atomicAdd(a.counters + 14 + k, (unsigned long long)itc[k]);
         }
     }
     __syncthreads();
@@ -1479,6 +1505,8 @@ struct pt_ctx {
     float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
     size_t pray_words = 0;
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
+    uint32_t wf_top = kTopNodesMax; // BVH4 nodes staged in each block's LDS (PT_WF_TOP; 0 = none)
+    uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
     int wf_pool = 0;                // paths per wave of the path-pool kernel (128 / 256), 0 = one per lane (PT_WF_POOL)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
@@ -1680,6 +1708,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
+        if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
         if (const char* e = getenv("PT_WF_POOL")) {
             const int v = atoi(e);
             c->wf_pool = (v == 128 || v == 256) ? v : 0;
@@ -1701,9 +1730,38 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
         lap("BVH4 collapse");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }
-        an.resize(acc4.nodes.size());
-        for (size_t i = 0; i < acc4.nodes.size(); ++i) {
-            const pt::Accel4Node& x = acc4.nodes[i];
+        // Node order: the kTopNodesMax nodes most likely to be visited first (best-first by box
+        // surface area from the root: a connected top subtree, staged in LDS by the wavefront
+        // kernel), then the others in their DFS order.
+        const uint32_t n4 = (uint32_t)acc4.nodes.size();
+        std::vector<uint32_t> new_of(n4, ~0u), old_of;
+        old_of.reserve(n4);
+        {
+            std::vector<std::pair<float, uint32_t>> heap{{INFINITY, 0u}};
+            while (!heap.empty() && old_of.size() < kTopNodesMax) {
+                std::pop_heap(heap.begin(), heap.end());
+                const uint32_t o = heap.back().second;
+                heap.pop_back();
+                new_of[o] = (uint32_t)old_of.size();
+                old_of.push_back(o);
+                const pt::Accel4Node& x = acc4.nodes[o];
+                for (int k = 0; k < 4; ++k) {
+                    if (x.child[k] == pt::kAccel4Empty || (x.child[k] & PT_BVH_LEAF_FLAG)) continue;
+                    const float b[6] = {x.lo[0][k], x.lo[1][k], x.lo[2][k], x.hi[0][k], x.hi[1][k], x.hi[2][k]};
+                    const float ex = b[3] - b[0], ey = b[4] - b[1], ez = b[5] - b[2];
+                    heap.push_back({ex * ey + ey * ez + ez * ex, x.child[k]});
+                    std::push_heap(heap.begin(), heap.end());
+                }
+            }
+            for (uint32_t o = 0; o < n4; ++o)
+                if (new_of[o] == ~0u) { new_of[o] = (uint32_t)old_of.size(); old_of.push_back(o); }
+        }
+        c->top_nodes = std::min(c->wf_top, n4);
+        an.resize(n4);
+        for (size_t i = 0; i < n4; ++i) {
+            pt::Accel4Node x = acc4.nodes[old_of[i]];
+            for (int k = 0; k < 4; ++k)
+                if (x.child[k] != pt::kAccel4Empty && !(x.child[k] & PT_BVH_LEAF_FLAG)) x.child[k] = new_of[x.child[k]];
             an[i].lox = make_float4(x.lo[0][0], x.lo[0][1], x.lo[0][2], x.lo[0][3]);
             an[i].loy = make_float4(x.lo[1][0], x.lo[1][1], x.lo[1][2], x.lo[1][3]);
             an[i].loz = make_float4(x.lo[2][0], x.lo[2][1], x.lo[2][2], x.lo[2][3]);
@@ -1714,7 +1772,12 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             an[i].pad = make_uint4(0u, 0u, 0u, 0u);
         }
         at.resize(nt);
-        for (uint32_t i = 0; i < nt; ++i) at[i] = tri_rec(acc.leaf_order[i]);
+        for (uint32_t i = 0; i < nt; ++i) {   // permuted for tri_hit_pk: {v0.xy, e1.xy}, {e2.xy, v0.z, e1.z}
+            const DTri r = tri_rec(acc.leaf_order[i]);
+            at[i].a = make_float4(r.a.x, r.a.y, r.a.w, r.b.x);
+            at[i].b = make_float4(r.b.z, r.b.w, r.a.z, r.b.y);
+            at[i].c = r.c;
+        }
         memcpy(c->acc_root, acc.root_box, sizeof(c->acc_root));
         c->acc4_depth = acc4.depth;
         uint32_t bits = 1;
@@ -1898,7 +1961,9 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         Args b = a;
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
-        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4;
+        b.top_nodes = c->top_nodes;
+        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
+                              (size_t)b.top_nodes * kTopNodeBytes;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         // Work units: whole pixels, unless the shard has too few pixels to keep every resident
         // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
@@ -2002,8 +2067,10 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 for (int k = 0; k < kSections; ++k) fprintf(f, " %llu", cnt[32 + k]);
                 fprintf(f, "\nwalk_hist");
                 for (int k = 0; k < kHist; ++k) fprintf(f, " %llu", cnt[32 + kSections + k]);
-                fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu start_wait %llu\n", cnt[11], cnt[5],
-                        cnt[2], cnt[6], cnt[12]);
+                fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu start_wait %llu top_visits %llu\n", cnt[11], cnt[5],
+                        cnt[2], cnt[6], cnt[12], cnt[13]);
+                fprintf(f, "iters_by_deep_lanes 0:%llu 1-4:%llu 5-8:%llu more:%llu no_leaf %llu neither %llu\n", cnt[14],
+                        cnt[15], cnt[16], cnt[17], cnt[18], cnt[19]);
                 fclose(f);
             }
         }
