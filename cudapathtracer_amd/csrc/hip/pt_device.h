@@ -626,12 +626,13 @@ struct Stack4 {
     uint32_t* spill_base;      // HBM (uniform)
     const uint32_t* lane_off;  // -> lane byte offset (a caller variable), & off_mask
     uint32_t off_mask;
+    uint32_t off_shift = 0;      // lane byte offset = (*lane_off & off_mask) >> off_shift
     uint32_t stride;
     const char* top = nullptr;   // LDS copy of BVH4 nodes 0..ntop-1 (kTopNodeBytes each), or none
     uint32_t ntop = 0;
     __device__ __forceinline__ uint32_t* spill() const
     {
-        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spill_base) + (*lane_off & off_mask));
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spill_base) + ((*lane_off & off_mask) >> off_shift));
     }
 };
 constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;

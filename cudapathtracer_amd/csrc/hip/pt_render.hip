@@ -522,52 +522,77 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
 // Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
 enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4, ST_CHECK = 5 };
 
-// Per-lane shading state ("cold": not needed while the lane walks) lives in HBM, word k of lane g
-// at cold[k * stride + g] (coalesced), and is loaded/stored only around the shading phase, so the
-// walk phase's register footprint is the ray, the walk state and the stack -- which is what sets
-// the kernel's occupancy.
+// Per-lane shading state ("cold": not needed while the lane walks) lives in HBM and is loaded /
+// stored only around the shading phase, so the walk phase's register footprint is the ray, the
+// walk state and the stack -- which is what sets the kernel's occupancy.
+// Layout: 16-B cells, lane-major within a cell row -- word w of record g at byte
+// ((w / 4) * records + g) * 16 + (w % 4) * 4 -- so the words a pass always needs come as four
+// coalesced 16-B-per-lane loads (and stores) instead of fifteen 4-B ones: a vector-memory
+// instruction costs about the same address-pipeline time at 4 and at 16 B per lane.
 enum : int {
-    CW_PX = 0, CW_PY, CW_N, CW_I, CW_FLAGS, CW_MTRI, CW_MT,
-    CW_RNG = 7,                       // d, v0..v4
-    CW_M = 13,                        // m0..m2 (f64, lo/hi words)
-    CW_ACC = 19,                      // acc (f64 x 3)
-    CW_WGT = 25,                      // wgt (f64 x 3)
-    CW_NEND = 31,                     // last sample number of the unit
-    CW_Q = 32,                        // pixel slot of the unit (per-sample buffer row)
-    CW_PST = 33,                      // path-pool kernel: path state (ST_*) while queued for shading
-    CW_CD = 34,                       // camera ray direction of a pinhole unit (f32 x 3, CF_CAMC)
-    kColdWords = 37
+    CW_N = 0, CW_I, CW_FLAGS, CW_RNG_D,       // cell 0
+    CW_RNG_V0 = 4,                            // cell 1: v0..v3
+    CW_WGT = 8,                               // cells 2, 3.lo: wgt (f64 x 3, lo/hi words)
+    CW_RNG_V4 = 14, CW_NEND = 15,             // cell 3.hi: v4, last sample number of the unit
+    CW_ACC = 16,                              // cells 4, 5.lo: acc (f64 x 3)
+    CW_M = 22,                                // cells 5.hi, 6: running mean m0..m2 (f64)
+    CW_PX = 28, CW_PY, CW_MTRI, CW_MT,        // cell 7: pixel, primary memo (tri, t)
+    CW_CD = 32,                               // cell 8: camera ray direction of a pinhole unit (CF_CAMC) ...
+    CW_Q = 35,                                //         ... and the unit's pixel slot (per-sample buffer row)
+    CW_PST = 36,                              // cell 9: path-pool kernel: path state while queued for shading
+    kColdWords = 40
 };
-// CF_OWNER: chunk 0 of a split pixel (publishes its primary hit in pmemo); CF_SHARE: a later
-// chunk (takes the published hit instead of tracing the camera ray again)
-// CF_MEMO: the pending hit came from the memo (already includes spheres)
-// CF_CAMC: the (sample-invariant, pinhole) camera direction is cached in CW_CD
 enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64 };
 
-// Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the word
-// offset k * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
+// Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the cell
+// offset (w / 4) * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
+// ld/st: one word; ld2/st2: words k, k+1 (k even); ld4/st4: a whole cell (k % 4 == 0).
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 struct ColdRec {
     __amdgpu_buffer_rsrc_t rs;
-    uint32_t voff;      // lane byte offset
-    uint32_t sbytes;    // bytes between consecutive words of one lane
+    uint32_t voff;      // lane byte offset (16 * record)
+    uint32_t sbytes;    // bytes between consecutive cells of one record (16 * records)
+    __device__ __forceinline__ int vo(int k) const { return (int)(voff + 4u * (uint32_t)(k & 3)); }
+    __device__ __forceinline__ int so(int k) const { return (int)((uint32_t)(k >> 2) * sbytes); }
     __device__ __forceinline__ uint32_t ld(int k) const
     {
-        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)((uint32_t)k * sbytes), 0);
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, vo(k), so(k), 0);
     }
     __device__ __forceinline__ void st(int k, uint32_t v) const
     {
-        __builtin_amdgcn_raw_buffer_store_b32((int)v, rs, (int)voff, (int)((uint32_t)k * sbytes), 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo(k), so(k), 0);
+    }
+    __device__ __forceinline__ uint2 ld2(int k) const
+    {
+        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo(k), so(k), 0);
+        return make_uint2(v.x, v.y);
+    }
+    __device__ __forceinline__ void st2(int k, uint32_t x, uint32_t y) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b64(u2v{x, y}, rs, vo(k), so(k), 0);
+    }
+    __device__ __forceinline__ uint4 ld4(int k) const
+    {
+        const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo(k), so(k), 0);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __device__ __forceinline__ void st4(int k, uint32_t x, uint32_t y, uint32_t z, uint32_t w) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{x, y, z, w}, rs, vo(k), so(k), 0);
     }
     __device__ __forceinline__ double ldd(int k) const
     {
-        return __hiloint2double((int)ld(k + 1), (int)ld(k));
+        const uint2 v = ld2(k);
+        return __hiloint2double((int)v.y, (int)v.x);
     }
     __device__ __forceinline__ void std_(int k, double v) const
     {
-        st(k, (uint32_t)__double2loint(v));
-        st(k + 1, (uint32_t)__double2hiint(v));
+        st2(k, (uint32_t)__double2loint(v), (uint32_t)__double2hiint(v));
     }
 };
+__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) { return __hiloint2double((int)hi, (int)lo); }
+__device__ __forceinline__ uint32_t dlo(double v) { return (uint32_t)__double2loint(v); }
+__device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hiint(v); }
 
 // kMinWaves: waves per SIMD the register allocation must allow (launch bound); 4 = 128 VGPRs,
 // 5 = 96, 6 = 80 -- more resident waves hide more memory latency, at the price of spilling
@@ -704,12 +729,14 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         htri = (int32_t)__float_as_uint(C.y);
         state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
     }
-    int n = (int)R.ld(CW_N), i = (int)R.ld(CW_I);
-    uint32_t fl = R.ld(CW_FLAGS);
+    // the words every pass needs: four 16-B cells
+    const uint4 k0 = R.ld4(CW_N), k1 = R.ld4(CW_RNG_V0), k2 = R.ld4(CW_WGT), k3 = R.ld4(CW_WGT + 4);
+    int n = (int)k0.x, i = (int)k0.y;
+    uint32_t fl = k0.z;
     Rng rng;
-    rng.d = R.ld(CW_RNG); rng.v0 = R.ld(CW_RNG + 1); rng.v1 = R.ld(CW_RNG + 2);
-    rng.v2 = R.ld(CW_RNG + 3); rng.v3 = R.ld(CW_RNG + 4); rng.v4 = R.ld(CW_RNG + 5);
-    C3 wgt = c3(R.ldd(CW_WGT), R.ldd(CW_WGT + 2), R.ldd(CW_WGT + 4));
+    rng.d = k0.w; rng.v0 = k1.x; rng.v1 = k1.y; rng.v2 = k1.z; rng.v3 = k1.w; rng.v4 = k3.z;
+    uint32_t nend = k3.w;
+    C3 wgt = c3(dbl(k2.x, k2.y), dbl(k2.z, k2.w), dbl(k3.x, k3.y));
 
     // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
     // a ray outside the Markstein preconditions, which takes the exact slow walk)
@@ -727,7 +754,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     // start sample n of pixel (px, py): camera ray, then memo or trace
     auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
         i = 0;
-        R.std_(CW_ACC, 0.0); R.std_(CW_ACC + 2, 0.0); R.std_(CW_ACC + 4, 0.0);
+        R.st4(CW_ACC, 0u, 0u, 0u, 0u); R.st2(CW_ACC + 4, 0u, 0u);
         wgt = c3(1, 1, 1);
         float u1 = 0.0f, u2 = 0.0f;
         const bool lens = (fl & CF_LENS) != 0u;
@@ -742,12 +769,14 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             }
         } else {
             ro = v3(0.0f, 0.0f, 0.0f) + v3(a.cam.pos[0], a.cam.pos[1], a.cam.pos[2]);   // as camera_ray forms it
-            rd = v3(__uint_as_float(R.ld(CW_CD)), __uint_as_float(R.ld(CW_CD + 1)), __uint_as_float(R.ld(CW_CD + 2)));
+            const uint4 cd = R.ld4(CW_CD);
+            rd = v3(__uint_as_float(cd.x), __uint_as_float(cd.y), __uint_as_float(cd.z));
         }
         wave_count(lcnt + 1, lane);
         if (fl & CF_HAVE) {
             SEC(SEC_MEMO);
-            htri = (int32_t)R.ld(CW_MTRI); ht = __uint_as_float(R.ld(CW_MT));
+            const uint2 mm = R.ld2(CW_MTRI);
+            htri = (int32_t)mm.x; ht = __uint_as_float(mm.y);
             fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
             return true;
         }
@@ -786,7 +815,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         fl &= ~CF_MEMO;
         if (fl & CF_PRIMARY) {
             fl = (fl | CF_HAVE) & ~CF_PRIMARY;
-            R.st(CW_MTRI, (uint32_t)htri); R.st(CW_MT, __float_as_uint(ht));
+            R.st2(CW_MTRI, (uint32_t)htri, __float_as_uint(ht));
             if (fl & CF_OWNER) {
                 const uint32_t q = R.ld(CW_Q);
                 a.pmemo[2 * (size_t)q + 1] = __float_as_uint(ht);
@@ -807,9 +836,11 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             const V3 normal = prim_normal(a, tri, pos);
             if (cm->emission[0] != 0) {
                 SEC(SEC_EMIT);
-                C3 acc = c3(R.ldd(CW_ACC), R.ldd(CW_ACC + 2), R.ldd(CW_ACC + 4));
+                const uint4 a01 = R.ld4(CW_ACC);
+                const uint2 a2 = R.ld2(CW_ACC + 4);
+                C3 acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2.x, a2.y));
                 acc = cadd(acc, cmul(wgt, mat_emission(cm)));
-                R.std_(CW_ACC, acc.r); R.std_(CW_ACC + 2, acc.g); R.std_(CW_ACC + 4, acc.b);
+                R.st4(CW_ACC, dlo(acc.r), dhi(acc.r), dlo(acc.g), dhi(acc.g)); R.st2(CW_ACC + 4, dlo(acc.b), dhi(acc.b));
                 wgt = c3(0, 0, 0);
             }
             // The two sampling branches (kernel.cu:470-497 light sample, 498-509 cosine) with their
@@ -889,12 +920,17 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             if (i >= D) {
                 wave_count(lcnt + 2, lane);
                 SEC(SEC_SAMPLE_END);
-                const uint32_t px = R.ld(CW_PX), py = R.ld(CW_PY);
+                const uint2 pxy = R.ld2(CW_PX);
+                const uint32_t px = pxy.x, py = pxy.y;
+                // acc and the running mean: cells 4..6 = acc.r, acc.g | acc.b, m0 | m1, m2
+                const uint4 a01 = R.ld4(CW_ACC), a2m0 = R.ld4(CW_ACC + 4);
+                const C3 acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2m0.x, a2m0.y));
                 if (a.chunks == 1) {
+                    const uint4 m12 = R.ld4(CW_M + 2);
                     const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
-                    const double m0 = (R.ldd(CW_M) * fn1) / fn + R.ldd(CW_ACC) / fn;
-                    const double m1 = (R.ldd(CW_M + 2) * fn1) / fn + R.ldd(CW_ACC + 2) / fn;
-                    const double m2 = (R.ldd(CW_M + 4) * fn1) / fn + R.ldd(CW_ACC + 4) / fn;
+                    const double m0 = (dbl(a2m0.z, a2m0.w) * fn1) / fn + acc.r / fn;
+                    const double m1 = (dbl(m12.x, m12.y) * fn1) / fn + acc.g / fn;
+                    const double m2 = (dbl(m12.z, m12.w) * fn1) / fn + acc.b / fn;
                     if (n >= a.spp) {
                         float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
                         o3[0] = (float)m0;
@@ -903,15 +939,15 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                         state = ST_IDLE;
                         break;
                     }
-                    R.std_(CW_M, m0); R.std_(CW_M + 2, m1); R.std_(CW_M + 4, m2);
+                    R.std_(CW_M, m0); R.st4(CW_M + 2, dlo(m1), dhi(m1), dlo(m2), dhi(m2));
                 } else {
                     // split pixel: keep L_n, finalize_pixels forms the ordered mean
                     const size_t ch = (size_t)a.spp * a.npix;
                     double* L = a.lbuf + (size_t)(n - 1) * a.npix + R.ld(CW_Q);
-                    L[0] = R.ldd(CW_ACC);
-                    L[ch] = R.ldd(CW_ACC + 2);
-                    L[2 * ch] = R.ldd(CW_ACC + 4);
-                    if ((uint32_t)n >= R.ld(CW_NEND)) {
+                    L[0] = acc.r;
+                    L[ch] = acc.g;
+                    L[2 * ch] = acc.b;
+                    if ((uint32_t)n >= nend) {
                         state = ST_IDLE;
                         break;
                     }
@@ -964,10 +1000,10 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                     if (a.chunks > 1 && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
                         fl |= (c == 0) ? CF_OWNER : CF_SHARE;
                     n = (int)chunk_first(a, c) + 1;
-                    R.st(CW_PX, px); R.st(CW_PY, py);
-                    R.st(CW_NEND, chunk_first(a, c + 1));
+                    R.st2(CW_PX, px, py);
+                    nend = chunk_first(a, c + 1);
                     R.st(CW_Q, q);
-                    R.std_(CW_M, 0.0); R.std_(CW_M + 2, 0.0); R.std_(CW_M + 4, 0.0);
+                    R.st2(CW_M, 0u, 0u); R.st4(CW_M + 2, 0u, 0u, 0u, 0u);
                     start_sample(px, py);
                 }
             }
@@ -975,10 +1011,10 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     }
 
     SEC(SEC_RECORD);
-    R.st(CW_N, (uint32_t)n); R.st(CW_I, (uint32_t)i); R.st(CW_FLAGS, fl);
-    R.st(CW_RNG, rng.d); R.st(CW_RNG + 1, rng.v0); R.st(CW_RNG + 2, rng.v1);
-    R.st(CW_RNG + 3, rng.v2); R.st(CW_RNG + 4, rng.v3); R.st(CW_RNG + 5, rng.v4);
-    R.std_(CW_WGT, wgt.r); R.std_(CW_WGT + 2, wgt.g); R.std_(CW_WGT + 4, wgt.b);
+    R.st4(CW_N, (uint32_t)n, (uint32_t)i, fl, rng.d);
+    R.st4(CW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
+    R.st4(CW_WGT, dlo(wgt.r), dhi(wgt.r), dlo(wgt.g), dhi(wgt.g));
+    R.st4(CW_WGT + 4, dlo(wgt.b), dhi(wgt.b), rng.v4, nend);
 }
 
 template <bool kCount, int kMinWaves>
@@ -1015,10 +1051,11 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.ring = lds_wf + (threadIdx.x >> 6) * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
     const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
-                    (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 4u, a.cold_stride * 4u};
-    S.spill_base = a.spill;   // spill column of lane g at byte offset 4g: R.voff
+                    (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16u, a.cold_stride * 16u};
+    S.spill_base = a.spill;   // spill column of lane g at byte offset 4g = R.voff / 4
     S.lane_off = &R.voff;
     S.off_mask = ~0u;
+    S.off_shift = 2;
     // the top of the BVH4 in LDS (after the rings and counters; kTopNodeBytes per node)
     float4* const ltop = reinterpret_cast<float4*>(lcnt + 4 + (kSections + kHist) / 2);
     for (uint32_t k = threadIdx.x; k < a.top_nodes * (kTopNodeBytes / 16); k += blockDim.x) {
@@ -1127,7 +1164,7 @@ template <int kPaths>
 __device__ __forceinline__ ColdRec path_rec(const Args& a, uint32_t g)
 {
     return ColdRec{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
-                   g * 4u, a.cold_stride * 4u};
+                   g * 16u, a.cold_stride * 16u};
 }
 
 template <bool kCount, int kMinWaves, int kPaths>
