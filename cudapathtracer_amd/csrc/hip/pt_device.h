@@ -349,6 +349,20 @@ __device__ __forceinline__ float rcp_or_inf(float d)
 {
     return (d == 0.0f) ? __builtin_copysignf(INFINITY, d) : rcp_rn(d);
 }
+// Double-precision Markstein quotient: with y = RN(1/d) (an IEEE division), q0 = RN(x*y),
+// r = x - d*q0 (exact by FMA), RN(q0 + r*y) == RN(x/d) for finite x, d without under/overflow.
+// quot_ok(x): x is 0 or 2^-969 <= |x| <= 2^1000, so that for the divisors used here (integers
+// 1..2^24) every quotient and intermediate is a normal double.
+__device__ __forceinline__ bool quot_ok(double x)
+{
+    const double ax = __builtin_fabs(x);
+    return x == 0.0 || (ax >= 0x1p-969 && ax <= 0x1p1000);
+}
+__device__ __forceinline__ double div_mk_d(double x, double d, double y)
+{
+    const double q0 = x * y;
+    return __builtin_fma(__builtin_fma(-q0, d, x), y, q0);
+}
 // div_mk for a divisor known to be nonzero
 __device__ __forceinline__ float div_mk_nz(float x, float d, float y)
 {

@@ -542,7 +542,9 @@ enum : int {
     CW_PST = 36,                              // cell 9: path-pool kernel: path state while queued for shading
     kColdWords = 40
 };
-enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64 };
+// CF_ACC0: the sample's accumulator is 0 (not yet written: the record's acc words are stale)
+enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64,
+                  CF_ACC0 = 128 };
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the cell
 // offset (w / 4) * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -754,7 +756,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     // start sample n of pixel (px, py): camera ray, then memo or trace
     auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
         i = 0;
-        R.st4(CW_ACC, 0u, 0u, 0u, 0u); R.st2(CW_ACC + 4, 0u, 0u);
+        fl |= CF_ACC0;   // acc = 0 (stored on the sample's first emission)
         wgt = c3(1, 1, 1);
         float u1 = 0.0f, u2 = 0.0f;
         const bool lens = (fl & CF_LENS) != 0u;
@@ -836,9 +838,13 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             const V3 normal = prim_normal(a, tri, pos);
             if (cm->emission[0] != 0) {
                 SEC(SEC_EMIT);
-                const uint4 a01 = R.ld4(CW_ACC);
-                const uint2 a2 = R.ld2(CW_ACC + 4);
-                C3 acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2.x, a2.y));
+                C3 acc = c3(0.0, 0.0, 0.0);
+                if (!(fl & CF_ACC0)) {
+                    const uint4 a01 = R.ld4(CW_ACC);
+                    const uint2 a2 = R.ld2(CW_ACC + 4);
+                    acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2.x, a2.y));
+                }
+                fl &= ~CF_ACC0;
                 acc = cadd(acc, cmul(wgt, mat_emission(cm)));
                 R.st4(CW_ACC, dlo(acc.r), dhi(acc.r), dlo(acc.g), dhi(acc.g)); R.st2(CW_ACC + 4, dlo(acc.b), dhi(acc.b));
                 wgt = c3(0, 0, 0);
@@ -923,14 +929,30 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 const uint2 pxy = R.ld2(CW_PX);
                 const uint32_t px = pxy.x, py = pxy.y;
                 // acc and the running mean: cells 4..6 = acc.r, acc.g | acc.b, m0 | m1, m2
-                const uint4 a01 = R.ld4(CW_ACC), a2m0 = R.ld4(CW_ACC + 4);
-                const C3 acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2m0.x, a2m0.y));
+                uint4 a01 = make_uint4(0u, 0u, 0u, 0u);
+                if (!(fl & CF_ACC0)) a01 = R.ld4(CW_ACC);
+                const uint4 a2m0 = R.ld4(CW_ACC + 4);   // (acc.b, only when !CF_ACC0) and m0
+                const C3 acc = (fl & CF_ACC0) ? c3(0.0, 0.0, 0.0)
+                                              : c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2m0.x, a2m0.y));
                 if (a.chunks == 1) {
                     const uint4 m12 = R.ld4(CW_M + 2);
                     const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
-                    const double m0 = (dbl(a2m0.z, a2m0.w) * fn1) / fn + acc.r / fn;
-                    const double m1 = (dbl(m12.x, m12.y) * fn1) / fn + acc.g / fn;
-                    const double m2 = (dbl(m12.z, m12.w) * fn1) / fn + acc.b / fn;
+                    const double x0 = dbl(a2m0.z, a2m0.w) * fn1, x1 = dbl(m12.x, m12.y) * fn1,
+                                 x2 = dbl(m12.z, m12.w) * fn1;
+                    double m0, m1, m2;
+                    // the six quotients by fn: one IEEE reciprocal + Markstein corrections (RN(x/fn)
+                    // for finite x clear of under/overflow -- else the whole wave divides)
+                    if (__ballot(!(quot_ok(x0) && quot_ok(x1) && quot_ok(x2) && quot_ok(acc.r) && quot_ok(acc.g) &&
+                                   quot_ok(acc.b))) == 0ull) {
+                        const double rf = 1.0 / fn;
+                        m0 = div_mk_d(x0, fn, rf) + div_mk_d(acc.r, fn, rf);
+                        m1 = div_mk_d(x1, fn, rf) + div_mk_d(acc.g, fn, rf);
+                        m2 = div_mk_d(x2, fn, rf) + div_mk_d(acc.b, fn, rf);
+                    } else {
+                        m0 = x0 / fn + acc.r / fn;
+                        m1 = x1 / fn + acc.g / fn;
+                        m2 = x2 / fn + acc.b / fn;
+                    }
                     if (n >= a.spp) {
                         float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
                         o3[0] = (float)m0;
