@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 NODE_BYTES = 128          # one BVH4 node record (6 x float4 child boxes + uint4 children + pad)
-ACCEL_TAG = "bvh4-hbmstate-v2"   # profiles/traffic.json is used only when it was measured on this kernel
+ACCEL_TAG = "bvh4-ldstop-cells-v3"   # profiles/traffic.json is used only when it was measured on this kernel
 
 
 def log(*a):
@@ -203,7 +203,7 @@ def main():
                     # algorithmic rate can exceed what HBM alone delivers (frac > 1); the HBM
                     # share is the measured traffic over the kernel time
                     "hbm_frac": (round(traffic / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
-                    "note": "algorithmic bytes include L2/MALL hits; the kernel is VALU-issue bound (DESIGN.md 6)",
+                    "note": "algorithmic bytes include L2/MALL hits; the kernel is co-bound by VALU issue and the per-lane vector-memory address pipeline (TA/TCP), not by HBM (DESIGN.md 6)",
                     "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_unidir_wf" if args.integrator == 0 and not (args.flags & 1) else "render_tiles",
                     "kernel_ms": round(kms, 3),
                     "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"]),

@@ -94,3 +94,22 @@ def test_c5_standin_4k_4096spp_depth16(standin):
     assert np.isfinite(img).all() and (img >= 0).all()
     assert st["samples"] == w * h * 4096
     _check(s, img, cam_kw, w, h, 4096, 16, _spread(w, h, 6, 4))
+
+
+@pytest.mark.parametrize("top", ["0", "1", "17"])
+def test_lds_top_nodes_bit_identical(standin, monkeypatch, top):
+    """The BVH4 top staged in LDS (PT_WF_TOP nodes; default 64) changes where node records are
+    read from, never the result: images with 0, 1 and 17 staged nodes equal the default's bit for
+    bit, and a spread of pixels equals the oracle."""
+    s, r = standin
+    w, h, spp = 320, 180, 8
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    cam = pt.make_camera(width=w, height=h, **cam_kw)
+    ref, _ = r.render(cam, w, h, spp, bounces=3)
+    monkeypatch.setenv("PT_WF_TOP", top)
+    with pt.Renderer(s, 0) as r2:
+        img, st = r2.render(cam, w, h, spp, bounces=3)
+    assert st["samples"] == w * h * spp
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    if top == "0":
+        _check(s, img, cam_kw, w, h, spp, 3, _spread(w, h, 32, 5))
