@@ -1786,6 +1786,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         lap("reference-BVH records");
         int rc4 = pt::build_accel(*sc, &acc);
         lap("SAH BVH build");
+        if (timing && rc4 == PT_OK) fprintf(stderr, "pt_create: render BVH SAH cost %.6g\n", pt::accel_sah_cost(acc));
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
         lap("BVH4 collapse");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }

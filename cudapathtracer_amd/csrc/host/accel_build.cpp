@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -219,7 +221,17 @@ struct ParallelBuild {
     }
 };
 
+
 }  // namespace
+
+double accel_sah_cost(const AccelBvh& acc)
+{
+    double c = 0.0;
+    for (const AccelNode& nd : acc.nodes)
+        for (int k = 0; k < 2; ++k)
+            if (!(nd.child[k] & PT_BVH_LEAF_FLAG)) c += surface(nd.box[k], nd.box[k] + 3);
+    return c + surface(acc.root_box, acc.root_box + 3);
+}
 
 int build_accel(const pt_scene& sc, AccelBvh* out)
 {
@@ -366,6 +378,8 @@ extern "C" int pt_accel_digest(const pt_scene* sc, uint64_t* digest, uint32_t* n
     int rc = pt::build_accel(*sc, &acc);
     if (rc == PT_OK) rc = pt::collapse_accel4(acc, &acc4);
     if (rc != PT_OK) return rc;
+    if (getenv("PT_TIMING")) fprintf(stderr, "pt_accel_digest: SAH cost %.6g, binary depth %d, BVH4 depth %d\n",
+                                     pt::accel_sah_cost(acc), acc.depth, acc4.depth);
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
         const unsigned char* c = static_cast<const unsigned char*>(p);

@@ -83,6 +83,8 @@ struct AccelBvh {
     float margin = 0.0f;
 };
 int build_accel(const pt_scene& sc, AccelBvh* out);
+// SAH cost of the binary tree: the sum of its inner-node surface areas (one triangle per leaf)
+double accel_sah_cost(const AccelBvh& acc);
 
 // 4-wide collapse of the binary SAH BVH: each node holds up to 4 children (largest-area
 // expansion), empty slots are kAccel4Empty; leaves stay single triangles (same leaf slots).
