@@ -475,22 +475,24 @@ __device__ __forceinline__ float tri_hit(V3 o, V3 d, const DTri* __restrict__ tr
 // Node of the render-path BVH4 (collapsed SAH BVH): 4 child boxes SoA + 4 child refs, 128 B.
 struct alignas(16) DNode4 {
     float4 lox, loy, loz, hix, hiy, hiz;
-    uint4 child;     // inner index, kLeaf | slot, or 0xffffffff (empty)
+    uint4 child;     // inner index, kLeaf | slot, or 0xffffffff (empty); leaf children first, with
+                     // consecutive triangle slots (child k of a node's leaves at slot base + k)
     uint4 pad;
 };
 static_assert(sizeof(DNode4) == 128, "BVH4 node is 128 B");
 constexpr uint32_t kEmpty = 0xffffffffu;
 constexpr uint32_t kNone = 0xffffffffu;    // no node / no leaf pending
-constexpr int kLeafRing = 8;               // LDS leaf-queue entries per lane
+constexpr int kLeafRing = 4;               // LDS leaf-queue entries per lane (one per node with entered leaves)
 constexpr int kRing = 16;                 // LDS stack entries per lane; deeper entries spill to HBM
 
 struct W4 {
     V3 inv;              // RN(1/d): also the Markstein reciprocal for the exact checks
     V3 oi;               // o * inv, for the conservative box test t = fma(b, inv, -oi)
     uint32_t node;       // next node to visit, kNone = pop one
-    uint32_t leaf;       // next leaf (triangle slot) to test, kNone = none pending
+    uint32_t leaf;       // leaves to test: (first slot << 4) | mask of entered leaf children; none
+                         // pending when the mask is 0 (leaf4_pending)
     int32_t sp;          // node stack depth
-    int32_t lsp;         // leaves queued in the LDS leaf ring (besides `leaf`)
+    int32_t lsp;         // leaf entries queued in the LDS leaf ring (besides `leaf`)
     float best_t;
     uint32_t best_slot;  // render-path triangle slot of the best hit, kNone = none
     uint32_t nx, ny, nz; // byte offsets in DNode4 of the near plane per axis (lo, or hi for inv < 0)
@@ -516,11 +518,21 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
     }
 }
 
+__device__ __forceinline__ bool leaf4_pending(const W4& w) { return (w.leaf & 15u) != 0u; }
+// the pending entry's lowest entered leaf slot (the mask is the low 4 bits: the word's lowest set
+// bit); an opaque v_ffbl so that the compiler recomputes it instead of keeping it live
+__device__ __forceinline__ uint32_t leaf4_slot(const W4& w)
+{
+    uint32_t b;
+    asm volatile("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(w.leaf));
+    return (w.leaf >> 4) + b;
+}
+
 // walk4_begin in two halves: the ray-independent reset, and the per-ray reciprocals / plane
 // offsets (the path-pool kernel runs the latter after the first node fetch is in flight).
 __device__ __forceinline__ void walk4_reset(W4& w)
 {
-    w.node = 0; w.leaf = kNone; w.sp = 0; w.lsp = 0;
+    w.node = 0; w.leaf = 0; w.sp = 0; w.lsp = 0;
     w.best_t = kMaxFloat; w.best_slot = kNone;
 }
 __device__ __forceinline__ void walk4_setup(W4& w, V3 o, V3 d)
@@ -655,7 +667,9 @@ constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
 // consecutive nodes occupy disjoint banks): lanes visiting them read LDS instead of issuing
 // vector-memory loads -- the kernel's limiting pipe (TA/TD, DESIGN.md "Measurement").
 constexpr uint32_t kTopNodeBytes = 112;
-constexpr uint32_t kTopNodesMax = 64;   // what fits next to the rings with 5 blocks of 256 threads per CU (66 does not)
+// what fits next to the rings with 5 blocks of 256 threads per CU: LDS is granted in 1280-B granules,
+// 32000 B per block = 4 x 5120 B of rings + 160 B of counters + 101 x 112 B
+constexpr uint32_t kTopNodesMax = 101;
 
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
 {
@@ -691,10 +705,10 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
                                            const Setup& setup = Setup())
 {
-    const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 4);
-    const bool leaf = w.leaf != kNone;
+    const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 1);
+    const bool leaf = leaf4_pending(w);
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
-    const uint32_t tb = mul48(leaf ? w.leaf : 0u);
+    const uint32_t tb = mul48(leaf ? leaf4_slot(w) : 0u);
     float4 A = ld_f4(tris, tb), B = ld_f4(tris, tb + 16u);
     float e2z = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tris) + tb + 32u);
     // a lane with no node to visit reads node 0 (the LDS copy when there is one)
@@ -725,14 +739,15 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
         const float t = tri_hit_pk(f2{o.x, o.y}, o.z, f2{d.x, d.y}, d.z, A, B, e2z);
+        const uint32_t lslot = leaf4_slot(w);   // (recomputed here: one register less across the loads)
         // ties go to the lower reference DFS rank (the reference's first-visited); exact ties are
         // rare, so both ranks are read only then
         if (0.0f < t && (t < w.best_t ||
                          (t == w.best_t && w.best_slot != kNone &&
-                          __float_as_uint(tris[w.leaf].c.z) < __float_as_uint(tris[w.best_slot].c.z)))) {
-            w.best_t = t; w.best_slot = w.leaf;
+                          __float_as_uint(tris[lslot].c.z) < __float_as_uint(tris[w.best_slot].c.z)))) {
+            w.best_t = t; w.best_slot = lslot;
         }
-        w.leaf = kNone;
+        w.leaf &= w.leaf - 1u;   // that leaf is done
     }
     if (visit) {
         const float lim = w.best_t * cull_rel;
@@ -743,24 +758,25 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
                    lim, cull_abs, t2, t3);
         uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
-        auto queue = [&](uint32_t slot) {
-            if (w.leaf == kNone) { w.leaf = slot; return; }
-            S.ring[(kRing + w.lsp) * 64] = slot;
-            ++w.lsp;
-        };
-        if ((r0 & kLeaf) && t0 != INFINITY) queue(r0 ^ kLeaf);
-        if ((r1 & kLeaf) && t1 != INFINITY) queue(r1 ^ kLeaf);
-        if ((r2 & kLeaf) && t2 != INFINITY) queue(r2 ^ kLeaf);
-        if ((r3 & kLeaf) && t3 != INFINITY) queue(r3 ^ kLeaf);
+        // entered leaf children as one queue entry: their slots are consecutive from child 0's
+        // (leaf children come first), so the entry is child 0's slot and a 4-bit mask
+        // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
+        const bool e0 = t0 != INFINITY, e1 = t1 != INFINITY, e2 = t2 != INFINITY, e3 = t3 != INFINITY;
+        const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
+        const uint32_t lm = (e0 && l0 ? 1u : 0u) | (e1 && l1 ? 2u : 0u) | (e2 && l2 ? 4u : 0u) | (e3 && l3 ? 8u : 0u);
+        if (lm != 0u) {
+            const uint32_t e = (r0 << 4) | lm;   // (the kLeaf bit shifts out)
+            if (!leaf4_pending(w)) w.leaf = e;
+            else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
+        }
         // inner children, nearest first.  Each entered inner child becomes its stack entry
         // (max(entry, 0) truncated to the bits above node_mask | node index): non-negative floats
         // order like their bit patterns, so four u32 min/max pairs sort the entries by distance;
         // leaves and boxes not entered become ~0 and sort last.
-        auto key = [&](float t, uint32_t r) -> uint32_t {
-            return ((r & kLeaf) || t == INFINITY) ? kNone
-                                                  : (((uint32_t)max((int32_t)__float_as_uint(t), 0) & ~node_mask) | r);
+        auto key = [&](float t, uint32_t r, bool e, bool l) -> uint32_t {
+            return (e && !l) ? (((uint32_t)max((int32_t)__float_as_uint(t), 0) & ~node_mask) | r) : kNone;
         };
-        uint32_t k0 = key(t0, r0), k1 = key(t1, r1), k2 = key(t2, r2), k3 = key(t3, r3);
+        uint32_t k0 = key(t0, r0, e0, l0), k1 = key(t1, r1, e1, l1), k2 = key(t2, r2, e2, l2), k3 = key(t3, r3, e3, l3);
         auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };
         ksort(k0, k1); ksort(k2, k3); ksort(k0, k2); ksort(k1, k3); ksort(k1, k2);
         if (__ballot(w.sp > kRing - 3) == 0ull) {
@@ -780,7 +796,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         }
         w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
     }
-    if (w.leaf == kNone && w.lsp > 0) {
+    if (!leaf4_pending(w) && w.lsp > 0) {
         --w.lsp;
         w.leaf = S.ring[(kRing + w.lsp) * 64];
     }
@@ -792,7 +808,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             break;
         }
     }
-    return w.node != kNone || w.leaf != kNone;
+    return w.node != kNone || leaf4_pending(w);
 }
 
 // Exact walk for the rare rays the fast path does not take (outside the Markstein

@@ -1103,9 +1103,9 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 if (state == ST_TRACE) ++trace_slots;
                 // wave iterations by the number of lanes needing a global node fetch (0, 1-4, 5-8,
                 // more), with no pending leaf in the wave, and with neither
-                const bool vis = state == ST_TRACE && w.node != kNone && w.lsp <= kLeafRing - 4;
+                const bool vis = state == ST_TRACE && w.node != kNone && w.lsp <= kLeafRing - 1;
                 const uint32_t deep = (uint32_t)__popcll(__ballot(vis && w.node >= S.ntop));
-                const bool noleaf = __ballot(state == ST_TRACE && w.leaf != kNone) == 0ull;
+                const bool noleaf = __ballot(state == ST_TRACE && leaf4_pending(w)) == 0ull;
                 ++itc[deep == 0u ? 0 : deep <= 4u ? 1 : deep <= 8u ? 2 : 3];
                 if (noleaf) ++itc[4];
                 if (noleaf && deep == 0u) ++itc[5];
@@ -1818,8 +1818,26 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         }
         c->top_nodes = std::min(c->wf_top, n4);
         an.resize(n4);
+        // Triangle slots: the leaf children of each node (in node order) get consecutive slots, and
+        // each node lists its leaf children first -- the walk queues a node's entered leaves as one
+        // entry (first slot, 4-bit mask).  slot_leaf[s] = the binary BVH's leaf slot.
+        std::vector<uint32_t> slot_leaf;
+        slot_leaf.reserve(nt);
         for (size_t i = 0; i < n4; ++i) {
-            pt::Accel4Node x = acc4.nodes[old_of[i]];
+            pt::Accel4Node x0 = acc4.nodes[old_of[i]], x = x0;
+            auto is_leaf = [](uint32_t r) { return r != pt::kAccel4Empty && (r & PT_BVH_LEAF_FLAG); };
+            int order[4], m = 0;
+            for (int k = 0; k < 4; ++k) if (is_leaf(x0.child[k])) order[m++] = k;
+            for (int k = 0; k < 4; ++k) if (!is_leaf(x0.child[k])) order[m++] = k;
+            for (int k = 0; k < 4; ++k) {
+                const int q = order[k];
+                for (int ax = 0; ax < 3; ++ax) { x.lo[ax][k] = x0.lo[ax][q]; x.hi[ax][k] = x0.hi[ax][q]; }
+                x.child[k] = x0.child[q];
+                if (is_leaf(x.child[k])) {
+                    slot_leaf.push_back(x.child[k] ^ PT_BVH_LEAF_FLAG);
+                    x.child[k] = PT_BVH_LEAF_FLAG | (uint32_t)(slot_leaf.size() - 1);
+                }
+            }
             for (int k = 0; k < 4; ++k)
                 if (x.child[k] != pt::kAccel4Empty && !(x.child[k] & PT_BVH_LEAF_FLAG)) x.child[k] = new_of[x.child[k]];
             an[i].lox = make_float4(x.lo[0][0], x.lo[0][1], x.lo[0][2], x.lo[0][3]);
@@ -1831,9 +1849,10 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             an[i].child = make_uint4(x.child[0], x.child[1], x.child[2], x.child[3]);
             an[i].pad = make_uint4(0u, 0u, 0u, 0u);
         }
+        if (slot_leaf.size() != nt) { delete c; return bail(pt::fail(PT_E_SCENE, "pt_create: BVH4 reaches %zu of %u triangles", slot_leaf.size(), nt)); }
         at.resize(nt);
         for (uint32_t i = 0; i < nt; ++i) {   // permuted for tri_hit_pk: {v0.xy, e1.xy}, {e2.xy, v0.z, e1.z}
-            const DTri r = tri_rec(acc.leaf_order[i]);
+            const DTri r = tri_rec(acc.leaf_order[slot_leaf[i]]);
             at[i].a = make_float4(r.a.x, r.a.y, r.a.w, r.b.x);
             at[i].b = make_float4(r.b.z, r.b.w, r.a.z, r.b.y);
             at[i].c = r.c;
