@@ -699,7 +699,8 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 struct NoSetup {
     __device__ void operator()(W4&) const {}
 };
-template <bool kCount, class Setup = NoSetup>
+// kTop: the caller guarantees S.ntop >= 1 (no per-step test of an empty LDS top).
+template <bool kCount, bool kTop = false, class Setup = NoSetup>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
@@ -719,8 +720,8 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     // deep nodes' lanes overwrite it with their global loads -- in this order, because the loads
     // write the same registers and an LDS read issued behind outstanding global loads to them
     // would have to wait out their whole latency.
-    if (S.ntop != 0u) {
-        const char* const lb = S.top + (nidx < S.ntop ? nidx : 0u) * kTopNodeBytes;
+    if (kTop || S.ntop != 0u) {
+        const char* const lb = S.top + __umul24(nidx < S.ntop ? nidx : 0u, kTopNodeBytes);   // (full-rate multiply)
         NX = lds_f4(lb, w.nx); FX = lds_f4(lb, w.nx ^ 48u);
         NY = lds_f4(lb, w.ny); FY = lds_f4(lb, w.ny ^ 80u);
         NZ = lds_f4(lb, w.nz); FZ = lds_f4(lb, w.nz ^ 112u);

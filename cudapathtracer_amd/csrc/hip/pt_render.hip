@@ -1111,8 +1111,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 if (noleaf && deep == 0u) ++itc[5];
             }
             if (state == ST_TRACE) {
-                const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
-                                                     a.node_mask, cnt);
+                const bool more = walk4_step<kCount, true>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
+                                                           a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
                     atomicAdd(lhist + min(31 - __clz((int)steps), kHist - 1), 1u);
@@ -1816,7 +1816,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             for (uint32_t o = 0; o < n4; ++o)
                 if (new_of[o] == ~0u) { new_of[o] = (uint32_t)old_of.size(); old_of.push_back(o); }
         }
-        c->top_nodes = std::min(c->wf_top, n4);
+        c->top_nodes = std::min(std::max(c->wf_top, 1u), n4);   // (>= 1: the wavefront walk reads the LDS top unconditionally)
         an.resize(n4);
         // Triangle slots: the leaf children of each node (in node order) get consecutive slots, and
         // each node lists its leaf children first -- the walk queues a node's entered leaves as one
