@@ -68,10 +68,13 @@ struct Args {
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
     const uint32_t* pix_states;     // XORWOW v0..v4, d of each work unit, word k of unit u at [k*nunits + u]
     uint32_t npix;                  // pixel slots of this shard (ntiles_shard * 64)
-    uint32_t chunks;                // sample chunks per pixel: unit u = chunk u / npix of slot u % npix
-    uint32_t* pmemo;                // chunks > 1: primary hit of pixel slot q: [2q] = tri + 2 (0 = not yet), [2q+1] = t
-    double* lbuf;                   // chunks > 1: per-sample radiance, channel k of sample n of pixel slot q
-                                    // at lbuf[(k * spp + n-1) * npix + q]
+    uint32_t nwhole;                // slots 0..nwhole-1 are whole-pixel units (unit u = slot u); the
+    uint32_t ntail;                 // ntail = npix - nwhole last slots are split into `chunks` sample
+    uint32_t chunks;                // chunks: unit nwhole + c * ntail + t = chunk c of slot nwhole + t
+    uint32_t* pmemo;                // split slots: primary hit of tail slot t as one 64-bit word: lo = tri + 2
+                                    // (0 = not yet), hi = t
+    double* lbuf;                   // split slots: per-sample radiance, channel k of sample n of tail slot t
+                                    // at lbuf[(k * spp + n-1) * ntail + t]
     const float4* spheres;          // sphere primitives: center xyz, radius (hit ids num_tris + i)
     uint32_t num_spheres;
     uint32_t num_tris;
@@ -538,13 +541,13 @@ enum : int {
     CW_M = 22,                                // cells 5.hi, 6: running mean m0..m2 (f64)
     CW_PX = 28, CW_PY, CW_MTRI, CW_MT,        // cell 7: pixel, primary memo (tri, t)
     CW_CD = 32,                               // cell 8: camera ray direction of a pinhole unit (CF_CAMC) ...
-    CW_Q = 35,                                //         ... and the unit's pixel slot (per-sample buffer row)
+    CW_Q = 35,                                //         ... and a split unit's tail slot (per-sample buffer row)
     CW_PST = 36,                              // cell 9: path-pool kernel: path state while queued for shading
     kColdWords = 40
 };
 // CF_ACC0: the sample's accumulator is 0 (not yet written: the record's acc words are stale)
 enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64,
-                  CF_ACC0 = 128 };
+                  CF_ACC0 = 128, CF_SPLIT = 256 };
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the cell
 // offset (w / 4) * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -647,10 +650,11 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     Rng r;
     rng_init(r, a.seed, idx, a.jump);
     const bool lens = (idx == 0) || (a.cam.radius != 0.0f);
+    const bool split = q >= a.nwhole;
     uint32_t done = 0;
-    for (uint32_t c = 0; c < a.chunks; ++c) {
+    for (uint32_t c = 0; c < (split ? a.chunks : 1u); ++c) {
         for (const uint32_t s0 = chunk_first(a, c); done < s0; ++done) replay_sample(r, lens, a.bounces);
-        const size_t u = (size_t)c * a.npix + q;
+        const size_t u = split ? (size_t)a.nwhole + (size_t)c * a.ntail + (q - a.nwhole) : (size_t)q;
         st[u] = r.v0;
         st[(size_t)a.nunits + u] = r.v1;
         st[2 * (size_t)a.nunits + u] = r.v2;
@@ -660,19 +664,19 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     }
 }
 
-// chunks > 1: the running mean of kernel.cu:551-552, in sample order, over the stored
-// per-sample radiance of each pixel of this shard.
+// Split slots: the running mean of kernel.cu:551-552, in sample order, over the stored
+// per-sample radiance of each split pixel of this shard.
 __global__ __launch_bounds__(256) void finalize_pixels(Args a)
 {
-    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    if (q >= a.npix) return;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= a.ntail) return;
     uint32_t px, py;
-    if (!unit_pixel(a, q, &px, &py)) return;
+    if (!unit_pixel(a, a.nwhole + t, &px, &py)) return;
     const size_t pix = (size_t)py * (size_t)a.w + px;
-    const size_t ch = (size_t)a.spp * a.npix;   // channel stride
-    const double* L = a.lbuf + q;
+    const size_t ch = (size_t)a.spp * a.ntail;   // channel stride
+    const double* L = a.lbuf + t;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-    for (int n = 1; n <= a.spp; ++n, L += a.npix) {
+    for (int n = 1; n <= a.spp; ++n, L += a.ntail) {
         const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
         m0 = (m0 * fn1) / fn + L[0] / fn;
         m1 = (m1 * fn1) / fn + L[ch] / fn;
@@ -785,10 +789,13 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         if (fl & CF_SHARE) {
             // the pixel's chunk 0 may have published the (sample-invariant) primary hit
             const uint32_t q = R.ld(CW_Q);
-            const uint32_t tv = __hip_atomic_load(a.pmemo + 2 * (size_t)q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (tv != 0u) {
-                htri = (int32_t)(tv - 2u);
-                ht = __uint_as_float(a.pmemo[2 * (size_t)q + 1]);
+            // hit and flag in one word: a relaxed agent-scope load (coherent across the XCDs' L2s
+            // for this word) needs no acquire, i.e. no invalidation of this XCD's L2
+            const uint64_t mv = __hip_atomic_load(reinterpret_cast<uint64_t*>(a.pmemo) + q, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)mv != 0u) {
+                htri = (int32_t)((uint32_t)mv - 2u);
+                ht = __uint_as_float((uint32_t)(mv >> 32));
                 fl = (fl | CF_PRIMARY | CF_MEMO) & ~CF_SHARE;   // stores the unit memo on shading
                 state = ST_SHADE;
                 return true;
@@ -820,8 +827,9 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             R.st2(CW_MTRI, (uint32_t)htri, __float_as_uint(ht));
             if (fl & CF_OWNER) {
                 const uint32_t q = R.ld(CW_Q);
-                a.pmemo[2 * (size_t)q + 1] = __float_as_uint(ht);
-                __hip_atomic_store(a.pmemo + 2 * (size_t)q, (uint32_t)(htri + 2), __ATOMIC_RELEASE,
+                // (one relaxed 64-bit store: no release, i.e. no write-back of this XCD's L2)
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(a.pmemo) + q,
+                                   ((uint64_t)__float_as_uint(ht) << 32) | (uint32_t)(htri + 2), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 fl &= ~CF_OWNER;
             }
@@ -934,7 +942,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 const uint4 a2m0 = R.ld4(CW_ACC + 4);   // (acc.b, only when !CF_ACC0) and m0
                 const C3 acc = (fl & CF_ACC0) ? c3(0.0, 0.0, 0.0)
                                               : c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2m0.x, a2m0.y));
-                if (a.chunks == 1) {
+                if (!(fl & CF_SPLIT)) {
                     const uint4 m12 = R.ld4(CW_M + 2);
                     const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
                     const double x0 = dbl(a2m0.z, a2m0.w) * fn1, x1 = dbl(m12.x, m12.y) * fn1,
@@ -964,8 +972,8 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                     R.std_(CW_M, m0); R.st4(CW_M + 2, dlo(m1), dhi(m1), dlo(m2), dhi(m2));
                 } else {
                     // split pixel: keep L_n, finalize_pixels forms the ordered mean
-                    const size_t ch = (size_t)a.spp * a.npix;
-                    double* L = a.lbuf + (size_t)(n - 1) * a.npix + R.ld(CW_Q);
+                    const size_t ch = (size_t)a.spp * a.ntail;
+                    double* L = a.lbuf + (size_t)(n - 1) * a.ntail + R.ld(CW_Q);
                     L[0] = acc.r;
                     L[ch] = acc.g;
                     L[2 * ch] = acc.b;
@@ -1005,9 +1013,13 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
         if (state == ST_IDLE) {
             const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             if (u >= a.nunits) {
+                if (kCount) atomicMin(a.counters + 21, (unsigned long long)wall_clock64());   // queue drained
                 state = ST_DONE;
             } else {
-                const uint32_t c = u / a.npix, q = u - c * a.npix;
+                const bool split = u >= a.nwhole;
+                const uint32_t c = split ? (u - a.nwhole) / a.ntail : 0u;
+                const uint32_t tq = split ? (u - a.nwhole) - c * a.ntail : 0u;   // tail slot
+                const uint32_t q = split ? a.nwhole + tq : u;
                 uint32_t px, py;
                 if (unit_pixel(a, q, &px, &py)) {
                     const uint32_t idx = morton2(px, py);
@@ -1019,12 +1031,13 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                     rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
                     rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
                     fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
-                    if (a.chunks > 1 && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
+                    if (split) fl |= CF_SPLIT;
+                    if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
                         fl |= (c == 0) ? CF_OWNER : CF_SHARE;
                     n = (int)chunk_first(a, c) + 1;
                     R.st2(CW_PX, px, py);
-                    nend = chunk_first(a, c + 1);
-                    R.st(CW_Q, q);
+                    nend = split ? chunk_first(a, c + 1) : (uint32_t)a.spp;
+                    R.st(CW_Q, tq);
                     R.st2(CW_M, 0u, 0u); R.st4(CW_M + 2, 0u, 0u, 0u, 0u);
                     start_sample(px, py);
                 }
@@ -1055,6 +1068,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     cnt.nodes = 0;
     cnt.tris = 0;
     cnt.leaf_steps = 0;
+    if (kCount && threadIdx.x == 0) atomicMin(a.counters + 20, (unsigned long long)wall_clock64());   // first start
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
     uint32_t trace_slots = 0, steps = 0;        // counting variant: lanes tracing per iteration; steps of this walk
     uint32_t start_wait = 0;                    // counting variant: lanes without a ray when a walk phase starts
@@ -1136,12 +1150,20 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // index, bounce, flags, RNG, path weight); accumulator, running mean, pixel and memo
         // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
-        if (state != ST_TRACE && state != ST_DONE) shade_lane<kCount>(a, R, lane, state, ro, rd, htri, ht, w, S, lcnt);
+        // (the lane id is recomputed for the shading pass: one VGPR less live across the walk loop)
+        if (state != ST_TRACE && state != ST_DONE)
+            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
     if (kCount) {
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
+        if (lane == 0) {   // wave exit times (wall clock): last, and the sum for the mean
+            const unsigned long long t = wall_clock64();
+            atomicMax(a.counters + 22, t);
+            atomicAdd(a.counters + 23, t);
+            atomicAdd(a.counters + 24, 1ull);
+        }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
         const unsigned long long c13 = wave_sum(cnt.top);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
@@ -1355,6 +1377,12 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
     }
     if (kCount) {
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
+        if (lane == 0) {   // wave exit times (wall clock): last, and the sum for the mean
+            const unsigned long long t = wall_clock64();
+            atomicMax(a.counters + 22, t);
+            atomicAdd(a.counters + 23, t);
+            atomicAdd(a.counters + 24, 1ull);
+        }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
         if (lane == 0) {
@@ -1561,6 +1589,9 @@ struct pt_ctx {
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
+    int wf_tail_chunks = 6;         // chunks of each tail pixel (PT_WF_TAIL_CHUNKS; 1 = no tail split)
+    double wf_tail_px = 0.75;       // tail pixels per resident lane (PT_WF_TAIL_PX)
+    int64_t wf_tail_npix = -1;      // explicit number of tail pixel slots (PT_WF_TAIL_NPIX), -1 = by wf_tail_px
     float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
     size_t pray_words = 0;
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
@@ -1766,6 +1797,9 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_TAIL_CHUNKS")) c->wf_tail_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_TAIL_PX")) c->wf_tail_px = std::max(0.0, atof(e));
+        if (const char* e = getenv("PT_WF_TAIL_NPIX")) c->wf_tail_npix = atoll(e);
         if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
         if (const char* e = getenv("PT_WF_POOL")) {
@@ -2028,6 +2062,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam;
     HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
     const uint32_t waves_per_cu = 16;
@@ -2044,25 +2079,41 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
                               (size_t)b.top_nodes * kTopNodeBytes;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
-        // Work units: whole pixels, unless the shard has too few pixels to keep every resident
-        // lane busy to the end (a pixel's samples run in sequence, so the kernel lasts at least
-        // one pixel's time): then each pixel is split into sample chunks.
+        // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
+        // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`
+        // pixel slots are split into sample chunks, so the final units are short.
+        // A shard with too few pixels to keep every resident lane busy is split entirely.
         b.npix = a.ntiles_shard * 64u;
         const uint32_t pool = (uint32_t)c->wf_pool;   // (pool kernels: 5 waves per SIMD)
         const uint32_t paths_per_block = pool ? 4u * pool : 256u;
         const uint64_t lanes = (uint64_t)blocks * paths_per_block;   // concurrently running paths
-        uint32_t chunks = 1;
-        if (c->wf_chunks > 0) chunks = (uint32_t)c->wf_chunks;
-        else if (2 * (uint64_t)b.npix < 5 * lanes) chunks = (uint32_t)((24 * lanes + b.npix - 1) / b.npix);
+        uint32_t chunks = 1, ntail = 0;
+        if (c->wf_tail_npix >= 0) {   // (tests: an explicit tail)
+            chunks = (uint32_t)(c->wf_chunks > 0 ? c->wf_chunks : c->wf_tail_chunks);
+            ntail = (uint32_t)std::min<int64_t>(b.npix, c->wf_tail_npix);
+        } else if (c->wf_chunks > 0) {
+            chunks = (uint32_t)c->wf_chunks;
+            ntail = b.npix;
+        } else if (2 * (uint64_t)b.npix < 5 * lanes) {
+            chunks = (uint32_t)((24 * lanes + b.npix - 1) / b.npix);
+            ntail = b.npix;
+        } else if (c->wf_tail_chunks > 1) {
+            // (measured on C3: +6% with 0.5..1 tail pixel per lane in 4..8 chunks; 0.75 x 6)
+            chunks = (uint32_t)c->wf_tail_chunks;
+            ntail = (uint32_t)std::min<uint64_t>(b.npix, (uint64_t)(c->wf_tail_px * (double)lanes));
+        }
         // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~24 units per lane)
         if (chunks > (uint32_t)p->spp) chunks = (uint32_t)p->spp;
-        if ((uint64_t)b.npix * chunks > 0xffffffffull) chunks = 1;
+        if ((uint64_t)b.npix + (uint64_t)ntail * (chunks - 1) > 0xffffffffull) chunks = 1;
+        if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; }
         b.chunks = chunks;
-        b.nunits = b.npix * chunks;
+        b.ntail = ntail;
+        b.nwhole = b.npix - ntail;
+        b.nunits = b.nwhole + ntail * chunks;
         const uint32_t need = (b.nunits + paths_per_block - 1) / paths_per_block;
         if (blocks > need) blocks = need;
-        if (chunks > 1) {
-            const size_t lw = (size_t)b.npix * (size_t)p->spp * 3;
+        if (ntail > 0) {
+            const size_t lw = (size_t)ntail * (size_t)p->spp * 3;
             if (c->lbuf_words < lw) {
                 if (c->lbuf) (void)hipFree(c->lbuf);
                 c->lbuf = nullptr;
@@ -2071,7 +2122,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 c->lbuf_words = lw;
             }
             b.lbuf = c->lbuf;
-            const size_t mw = (size_t)b.npix * 2;
+            const size_t mw = (size_t)ntail * 2;
             if (c->pmemo_words < mw) {
                 if (c->pmemo) (void)hipFree(c->pmemo);
                 c->pmemo = nullptr;
@@ -2121,7 +2172,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());
-        if (b.chunks > 1) hipLaunchKernelGGL(finalize_pixels, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b);
+        if (b.ntail > 0) hipLaunchKernelGGL(finalize_pixels, dim3((b.ntail + 255) / 256), dim3(256), 0, stream, b);
         HIP_TRY(hipGetLastError());
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
@@ -2148,6 +2199,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 for (int k = 0; k < kHist; ++k) fprintf(f, " %llu", cnt[32 + kSections + k]);
                 fprintf(f, "\ntrace_slots %llu walk_slots %llu nodes %llu leaf_steps %llu start_wait %llu top_visits %llu\n", cnt[11], cnt[5],
                         cnt[2], cnt[6], cnt[12], cnt[13]);
+                fprintf(f, "wall_clock start %llu drained %llu last_exit %llu mean_exit %.1f waves %llu (ticks)\n", cnt[20], cnt[21],
+                        cnt[22], cnt[24] ? (double)cnt[23] / (double)cnt[24] : 0.0, cnt[24]);
                 fprintf(f, "iters_by_deep_lanes 0:%llu 1-4:%llu 5-8:%llu more:%llu no_leaf %llu neither %llu\n", cnt[14],
                         cnt[15], cnt[16], cnt[17], cnt[18], cnt[19]);
                 fclose(f);

@@ -150,6 +150,31 @@ def test_sample_chunk_units_bit_exact(oracle_mod, monkeypatch, chunks, radius):
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("tail,chunks,radius", [("100", "3", 0.0), ("1", "9", 0.0), ("383", "2", 0.05),
+                                               ("0", "4", 0.0)])
+def test_tail_split_units_bit_exact(oracle_mod, monkeypatch, tail, chunks, radius):
+    """Hybrid work units: whole pixels first, the last `tail` pixel slots split into sample chunks
+    (PT_WF_TAIL_NPIX / PT_WF_CHUNKS; by default the last 0.75 pixel per resident lane in 6 chunks
+    on large shards).  The split pixels' radiance is stored per sample and combined in order, the
+    whole ones keep their running mean in the record: the same image bits as the oracle."""
+    monkeypatch.setenv("PT_WF_TAIL_NPIX", tail)
+    monkeypatch.setenv("PT_WF_CHUNKS", chunks)
+    s = load_scene("cornell_blob")
+    w, h, spp = 24, 16, 9
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=3)
+        parts = np.zeros_like(img)
+        for k in range(2):
+            part, _ = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=2)
+            parts += part
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 0, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert _bits_equal(parts, img.astype(np.float64)) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+
+
 @pytest.mark.parametrize("pool", ["128", "256"])
 @pytest.mark.parametrize("chunks,radius,flags,bounces", [
     ("1", 0.0, 0, 3), ("3", 0.0, 0, 3), ("1", 0.05, pt.PT_FLAG_COUNT, 3),
