@@ -66,7 +66,7 @@ struct Args {
                                     // (o.x, o.y, o.z, d.x), (d.y, d.z, hit slot / id, hit t)
     float acc_root[6];
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
-    const uint32_t* pix_states;     // XORWOW v0..v4, d of each work unit, word k of unit u at [k*nunits + u]
+    const uint32_t* pix_states;     // per work unit u, word k at [k*nunits + u] (kUnitWords, init_pixel_states)
     uint32_t npix;                  // pixel slots of this shard (ntiles_shard * 64)
     uint32_t nwhole;                // slots 0..nwhole-1 are whole-pixel units (unit u = slot u); the
     uint32_t ntail;                 // ntail = npix - nwhole last slots are split into `chunks` sample
@@ -414,10 +414,20 @@ __device__ C3 radiance_head(const Args& a, Tracer<kRefWalk, kCount>& tr, V3 cam_
 }
 
 // ------------------------------------------------------------------ camera (camera.h:77-97)
+// A kernel-argument value made opaque at its use, so that the compiler derives what it needs from
+// it there (e.g. a conversion) instead of hoisting the result out of the persistent loop into
+// registers that stay live across the walk (where they cost spills).
+template <typename T>
+__device__ __forceinline__ T fresh(T x)
+{
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
 __device__ __forceinline__ void camera_ray(const Cam& cam, uint32_t px, uint32_t py, bool lens, float u1, float u2,
                                            V3* o, V3* d)
 {
-    V3 film = v3((float)px / (float)cam.w - 0.5f, (float)py / (float)cam.h - 0.5f, 0.0f);
+    V3 film = v3((float)px / (float)fresh(cam.w) - 0.5f, (float)py / (float)fresh(cam.h) - 0.5f, 0.0f);
     V3 lo = v3(0.0f, 0.0f, 0.0f);
     if (lens) {
         const float r = cam.radius * sqrtf(u1);
@@ -604,6 +614,9 @@ __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hi
 // shading-phase values (the walk loop itself stays spill-free down to 96).
 // Work unit u = sample chunk c = u / npix of pixel slot q = u % npix: samples
 // [c*spp/chunks, (c+1)*spp/chunks).  With one chunk a unit is a whole pixel.
+// Per-unit words of init_pixel_states' output beyond the XORWOW state (words 0..5: v0..v4, d)
+enum : uint32_t { UW_PXY = 6, UW_N0, UW_NEND, UW_TQ, UW_CD, kUnitWords = UW_CD + 3 };
+constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the image
 __device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c)
 {
     return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / a.chunks);
@@ -641,26 +654,45 @@ __device__ __forceinline__ void replay_sample(Rng& rng, bool lens, int D)
 __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __restrict__ st)
 {
     // one lane per pixel slot: curand_init, then one pass over the samples that writes the state
-    // at the start of every chunk
+    // at the start of every chunk, with everything else a lane needs to start the unit (pixel,
+    // sample range, pinhole camera ray): the refill in the render kernel is then a few loads
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= a.npix) return;
+    const bool split = q >= a.nwhole;
+    const uint32_t nc = split ? a.chunks : 1u;
+    auto unit = [&](uint32_t c) -> size_t {
+        return split ? (size_t)a.nwhole + (size_t)c * a.ntail + (q - a.nwhole) : (size_t)q;
+    };
+    const size_t N = a.nunits;
     uint32_t px, py;
-    if (!unit_pixel(a, q, &px, &py)) return;
+    if (!unit_pixel(a, q, &px, &py)) {   // a slot outside the image (partial tile): no unit
+        for (uint32_t c = 0; c < nc; ++c) st[UW_PXY * N + unit(c)] = kNoPixel;
+        return;
+    }
     const uint32_t idx = morton2(px, py);
     Rng r;
     rng_init(r, a.seed, idx, a.jump);
     const bool lens = (idx == 0) || (a.cam.radius != 0.0f);
-    const bool split = q >= a.nwhole;
+    V3 o, d = v3(0.0f, 0.0f, 0.0f);
+    if (!lens) camera_ray(a.cam, px, py, false, 0.0f, 0.0f, &o, &d);   // the pixel's pinhole ray
     uint32_t done = 0;
-    for (uint32_t c = 0; c < (split ? a.chunks : 1u); ++c) {
-        for (const uint32_t s0 = chunk_first(a, c); done < s0; ++done) replay_sample(r, lens, a.bounces);
-        const size_t u = split ? (size_t)a.nwhole + (size_t)c * a.ntail + (q - a.nwhole) : (size_t)q;
+    for (uint32_t c = 0; c < nc; ++c) {
+        const uint32_t s0 = split ? chunk_first(a, c) : 0u;
+        for (; done < s0; ++done) replay_sample(r, lens, a.bounces);
+        const size_t u = unit(c);
         st[u] = r.v0;
-        st[(size_t)a.nunits + u] = r.v1;
-        st[2 * (size_t)a.nunits + u] = r.v2;
-        st[3 * (size_t)a.nunits + u] = r.v3;
-        st[4 * (size_t)a.nunits + u] = r.v4;
-        st[5 * (size_t)a.nunits + u] = r.d;       // the Weyl counter advances with every draw
+        st[N + u] = r.v1;
+        st[2 * N + u] = r.v2;
+        st[3 * N + u] = r.v3;
+        st[4 * N + u] = r.v4;
+        st[5 * N + u] = r.d;       // the Weyl counter advances with every draw
+        st[UW_PXY * N + u] = px | (py << 16);
+        st[UW_N0 * N + u] = (s0 + 1u) | (lens ? 0x80000000u : 0u);
+        st[UW_NEND * N + u] = split ? chunk_first(a, c + 1) : (uint32_t)a.spp;
+        st[UW_TQ * N + u] = split ? q - a.nwhole : 0u;
+        st[UW_CD * N + u] = __float_as_uint(d.x);
+        st[(UW_CD + 1) * N + u] = __float_as_uint(d.y);
+        st[(UW_CD + 2) * N + u] = __float_as_uint(d.z);
     }
 }
 
@@ -774,7 +806,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 fl |= CF_CAMC;
             }
         } else {
-            ro = v3(0.0f, 0.0f, 0.0f) + v3(a.cam.pos[0], a.cam.pos[1], a.cam.pos[2]);   // as camera_ray forms it
+            ro = v3(0.0f, 0.0f, 0.0f) + v3(fresh(a.cam.pos[0]), fresh(a.cam.pos[1]), fresh(a.cam.pos[2]));   // as camera_ray forms it
             const uint4 cd = R.ld4(CW_CD);
             rd = v3(__uint_as_float(cd.x), __uint_as_float(cd.y), __uint_as_float(cd.z));
         }
@@ -923,7 +955,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 i = (i > D - 2) ? i : D - 2;
             }
             C3 bw = cmulf(brdf(cm), f);
-            if (!cosb) bw = cmulf(bw, a.total_light_area);
+            if (!cosb) bw = cmulf(bw, fresh(a.total_light_area));
             wgt = cmul(wgt, bw);
             ro = pos;
             rd = ldir;
@@ -1016,28 +1048,31 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 if (kCount) atomicMin(a.counters + 21, (unsigned long long)wall_clock64());   // queue drained
                 state = ST_DONE;
             } else {
-                const bool split = u >= a.nwhole;
-                const uint32_t c = split ? (u - a.nwhole) / a.ntail : 0u;
-                const uint32_t tq = split ? (u - a.nwhole) - c * a.ntail : 0u;   // tail slot
-                const uint32_t q = split ? a.nwhole + tq : u;
-                uint32_t px, py;
-                if (unit_pixel(a, q, &px, &py)) {
-                    const uint32_t idx = morton2(px, py);
-                    // curand_init's state, computed for every unit by init_pixel_states
-                    rng.d = a.pix_states[5 * (size_t)a.nunits + u];
+                // the unit as init_pixel_states prepared it (pixel, sample range, curand_init's
+                // state fast-forwarded to the range, the pinhole camera ray)
+                const size_t N = a.nunits;
+                const uint32_t pxy = a.pix_states[UW_PXY * N + u];
+                if (pxy != kNoPixel) {
+                    const uint32_t px = pxy & 0xffffu, py = pxy >> 16;
+                    const uint32_t n0 = a.pix_states[UW_N0 * N + u];
                     rng.v0 = a.pix_states[u];
-                    rng.v1 = a.pix_states[(size_t)a.nunits + u];
-                    rng.v2 = a.pix_states[2 * (size_t)a.nunits + u];
-                    rng.v3 = a.pix_states[3 * (size_t)a.nunits + u];
-                    rng.v4 = a.pix_states[4 * (size_t)a.nunits + u];
-                    fl = ((idx == 0) || (a.cam.radius != 0.0f)) ? CF_LENS : 0u;
+                    rng.v1 = a.pix_states[N + u];
+                    rng.v2 = a.pix_states[2 * N + u];
+                    rng.v3 = a.pix_states[3 * N + u];
+                    rng.v4 = a.pix_states[4 * N + u];
+                    rng.d = a.pix_states[5 * N + u];
+                    nend = a.pix_states[UW_NEND * N + u];
+                    n = (int)(n0 & 0x7fffffffu);
+                    const bool split = u >= a.nwhole;
+                    fl = (n0 >> 31) ? CF_LENS : CF_CAMC;
+                    if (!(fl & CF_LENS))
+                        R.st4(CW_CD, a.pix_states[UW_CD * N + u], a.pix_states[(UW_CD + 1) * N + u],
+                              a.pix_states[(UW_CD + 2) * N + u], a.pix_states[UW_TQ * N + u]);
                     if (split) fl |= CF_SPLIT;
                     if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
-                        fl |= (c == 0) ? CF_OWNER : CF_SHARE;
-                    n = (int)chunk_first(a, c) + 1;
+                        fl |= (n == 1) ? CF_OWNER : CF_SHARE;   // (chunk 0 starts at sample 1)
                     R.st2(CW_PX, px, py);
-                    nend = split ? chunk_first(a, c + 1) : (uint32_t)a.spp;
-                    R.st(CW_Q, tq);
+                    if (split && (fl & CF_LENS)) R.st(CW_Q, a.pix_states[UW_TQ * N + u]);
                     R.st2(CW_M, 0u, 0u); R.st4(CW_M + 2, 0u, 0u, 0u, 0u);
                     start_sample(px, py);
                 }
@@ -1603,7 +1638,7 @@ struct pt_ctx {
     uint32_t* rparent = nullptr;
     uint32_t* spill = nullptr;
     size_t spill_words = 0;
-    uint32_t* pix_states = nullptr;   // init_pixel_states output (6 words per work unit)
+    uint32_t* pix_states = nullptr;   // init_pixel_states output (kUnitWords per work unit)
     size_t pix_states_words = 0;
     double* lbuf = nullptr;           // per-sample radiance of split pixels
     size_t lbuf_words = 0;
@@ -2060,7 +2095,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const float cam_ext = std::fmax(std::fabs(cam->pos.x), std::fmax(std::fabs(cam->pos.y), std::fabs(cam->pos.z)));
     const bool near_cam = cam_ext <= 64.0f * c->scene_extent;
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
-                           !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam;
+                           !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam &&
+                           p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
     HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
@@ -2151,7 +2187,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             }
             b.pray = c->pray;
         }
-        const size_t sw = (size_t)6 * b.nunits;
+        const size_t sw = (size_t)kUnitWords * b.nunits;
         if (c->pix_states_words < sw) {
             if (c->pix_states) (void)hipFree(c->pix_states);
             c->pix_states = nullptr;
