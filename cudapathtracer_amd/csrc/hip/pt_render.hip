@@ -2131,14 +2131,15 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             chunks = (uint32_t)c->wf_chunks;
             ntail = b.npix;
         } else if (2 * (uint64_t)b.npix < 5 * lanes) {
-            chunks = (uint32_t)((24 * lanes + b.npix - 1) / b.npix);
+            chunks = (uint32_t)((16 * lanes + b.npix - 1) / b.npix);
             ntail = b.npix;
         } else if (c->wf_tail_chunks > 1) {
             // (measured on C3: +6% with 0.5..1 tail pixel per lane in 4..8 chunks; 0.75 x 6)
             chunks = (uint32_t)c->wf_tail_chunks;
             ntail = (uint32_t)std::min<uint64_t>(b.npix, (uint64_t)(c->wf_tail_px * (double)lanes));
         }
-        // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~24 units per lane)
+        // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~16 units per lane:
+        // 1/8 shard 20 chunks, 1/4 shard 10)
         if (chunks > (uint32_t)p->spp) chunks = (uint32_t)p->spp;
         if ((uint64_t)b.npix + (uint64_t)ntail * (chunks - 1) > 0xffffffffull) chunks = 1;
         if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; }
