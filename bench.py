@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 NODE_BYTES = 128          # one BVH4 node record (6 x float4 child boxes + uint4 children + pad)
-ACCEL_TAG = "bvh4-ldstop-cells-v3"   # profiles/traffic.json is used only when it was measured on this kernel
+ACCEL_TAG = "bvh4-leafmask-tailsplit-v4"   # profiles/traffic.json is used only when it was measured on this kernel
 
 
 def log(*a):
