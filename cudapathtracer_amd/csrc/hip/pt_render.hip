@@ -69,8 +69,10 @@ struct Args {
     const uint32_t* pix_states;     // per work unit u, word k at [k*nunits + u] (kUnitWords, init_pixel_states)
     uint32_t npix;                  // pixel slots of this shard (ntiles_shard * 64)
     uint32_t nwhole;                // slots 0..nwhole-1 are whole-pixel units (unit u = slot u); the
-    uint32_t ntail;                 // ntail = npix - nwhole last slots are split into `chunks` sample
-    uint32_t chunks;                // chunks: unit nwhole + c * ntail + t = chunk c of slot nwhole + t
+    uint32_t ntail;                 // ntail = npix - nwhole last slots are split: the first nmid of them
+    uint32_t nmid;                  // into chunks_mid sample chunks, the rest into `chunks`; units are
+    uint32_t chunks_mid;            // numbered whole, then mid (chunk-major), then the rest (chunk-major)
+    uint32_t chunks;                // (init_pixel_states writes each unit's pixel and sample range)
     uint32_t* pmemo;                // split slots: primary hit of tail slot t as one 64-bit word: lo = tri + 2
                                     // (0 = not yet), hi = t
     double* lbuf;                   // split slots: per-sample radiance, channel k of sample n of tail slot t
@@ -617,9 +619,9 @@ __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hi
 // Per-unit words of init_pixel_states' output beyond the XORWOW state (words 0..5: v0..v4, d)
 enum : uint32_t { UW_PXY = 6, UW_N0, UW_NEND, UW_TQ, UW_CD, kUnitWords = UW_CD + 3 };
 constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the image
-__device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c)
+__device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c, uint32_t chunks)
 {
-    return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / a.chunks);
+    return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / chunks);
 }
 __device__ __forceinline__ bool unit_pixel(const Args& a, uint32_t q, uint32_t* px, uint32_t* py)
 {
@@ -659,9 +661,13 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= a.npix) return;
     const bool split = q >= a.nwhole;
-    const uint32_t nc = split ? a.chunks : 1u;
+    const uint32_t t = q - a.nwhole;   // split slot (row of the per-sample buffer)
+    const bool mid = split && t < a.nmid;
+    const uint32_t nc = !split ? 1u : mid ? a.chunks_mid : a.chunks;
     auto unit = [&](uint32_t c) -> size_t {
-        return split ? (size_t)a.nwhole + (size_t)c * a.ntail + (q - a.nwhole) : (size_t)q;
+        if (!split) return (size_t)q;
+        if (mid) return (size_t)a.nwhole + (size_t)c * a.nmid + t;
+        return (size_t)a.nwhole + (size_t)a.chunks_mid * a.nmid + (size_t)c * (a.ntail - a.nmid) + (t - a.nmid);
     };
     const size_t N = a.nunits;
     uint32_t px, py;
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     if (!lens) camera_ray(a.cam, px, py, false, 0.0f, 0.0f, &o, &d);   // the pixel's pinhole ray
     uint32_t done = 0;
     for (uint32_t c = 0; c < nc; ++c) {
-        const uint32_t s0 = split ? chunk_first(a, c) : 0u;
+        const uint32_t s0 = split ? chunk_first(a, c, nc) : 0u;
         for (; done < s0; ++done) replay_sample(r, lens, a.bounces);
         const size_t u = unit(c);
         st[u] = r.v0;
@@ -688,8 +694,8 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
         st[5 * N + u] = r.d;       // the Weyl counter advances with every draw
         st[UW_PXY * N + u] = px | (py << 16);
         st[UW_N0 * N + u] = (s0 + 1u) | (lens ? 0x80000000u : 0u);
-        st[UW_NEND * N + u] = split ? chunk_first(a, c + 1) : (uint32_t)a.spp;
-        st[UW_TQ * N + u] = split ? q - a.nwhole : 0u;
+        st[UW_NEND * N + u] = split ? chunk_first(a, c + 1, nc) : (uint32_t)a.spp;
+        st[UW_TQ * N + u] = split ? t : 0u;
         st[UW_CD * N + u] = __float_as_uint(d.x);
         st[(UW_CD + 1) * N + u] = __float_as_uint(d.y);
         st[(UW_CD + 2) * N + u] = __float_as_uint(d.z);
@@ -1627,6 +1633,10 @@ struct pt_ctx {
     int wf_tail_chunks = 6;         // chunks of each tail pixel (PT_WF_TAIL_CHUNKS; 1 = no tail split)
     double wf_tail_px = 0.75;       // tail pixels per resident lane (PT_WF_TAIL_PX)
     int64_t wf_tail_npix = -1;      // explicit number of tail pixel slots (PT_WF_TAIL_NPIX), -1 = by wf_tail_px
+    int wf_mid_chunks = -1;         // split shards: chunks of all but the last pixels (PT_WF_MID_CHUNKS;
+                                    // -1 = automatic, 0 or 1 = one split for all)
+    double wf_fine_px = 0.5;        // ... the last pixels per resident lane (PT_WF_FINE_PX)
+    int wf_fine_chunks = 0;         // ... and their chunks (PT_WF_FINE_CHUNKS; 0 = the automatic count)
     float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
     size_t pray_words = 0;
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
@@ -1835,6 +1845,9 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_TAIL_CHUNKS")) c->wf_tail_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_TAIL_PX")) c->wf_tail_px = std::max(0.0, atof(e));
         if (const char* e = getenv("PT_WF_TAIL_NPIX")) c->wf_tail_npix = atoll(e);
+        if (const char* e = getenv("PT_WF_MID_CHUNKS")) c->wf_mid_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_FINE_PX")) c->wf_fine_px = std::max(0.0, atof(e));
+        if (const char* e = getenv("PT_WF_FINE_CHUNKS")) c->wf_fine_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
         if (const char* e = getenv("PT_WF_POOL")) {
@@ -2123,7 +2136,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         const uint32_t pool = (uint32_t)c->wf_pool;   // (pool kernels: 5 waves per SIMD)
         const uint32_t paths_per_block = pool ? 4u * pool : 256u;
         const uint64_t lanes = (uint64_t)blocks * paths_per_block;   // concurrently running paths
-        uint32_t chunks = 1, ntail = 0;
+        uint32_t chunks = 1, ntail = 0, nmid = 0, chunks_mid = 1;
         if (c->wf_tail_npix >= 0) {   // (tests: an explicit tail)
             chunks = (uint32_t)(c->wf_chunks > 0 ? c->wf_chunks : c->wf_tail_chunks);
             ntail = (uint32_t)std::min<int64_t>(b.npix, c->wf_tail_npix);
@@ -2133,6 +2146,17 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         } else if (2 * (uint64_t)b.npix < 5 * lanes) {
             chunks = (uint32_t)((16 * lanes + b.npix - 1) / b.npix);
             ntail = b.npix;
+            // longer units first, the finer split for the last wf_fine_px pixels per lane
+            // (measured on C3 shards: 1/4 shard 3 mid chunks, 1/8 shard 6: +3..4% over one split)
+            const uint32_t nfine = (uint32_t)std::min<uint64_t>(b.npix, (uint64_t)(c->wf_fine_px * (double)lanes));
+            int mc = c->wf_mid_chunks;
+            if (mc < 0 && nfine < b.npix)   // automatic: ~2.5 mid units per lane, at most 6 chunks
+                mc = std::min(6, (int)std::ceil(2.5 * (double)lanes / (double)(b.npix - nfine)));
+            if (mc > 1 && nfine < b.npix) {
+                nmid = b.npix - nfine;
+                chunks_mid = (uint32_t)std::min(mc, p->spp);
+                if (c->wf_fine_chunks > 0) chunks = (uint32_t)c->wf_fine_chunks;
+            }
         } else if (c->wf_tail_chunks > 1) {
             // (measured on C3: +6% with 0.5..1 tail pixel per lane in 4..8 chunks; 0.75 x 6)
             chunks = (uint32_t)c->wf_tail_chunks;
@@ -2141,12 +2165,15 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~16 units per lane:
         // 1/8 shard 20 chunks, 1/4 shard 10)
         if (chunks > (uint32_t)p->spp) chunks = (uint32_t)p->spp;
-        if ((uint64_t)b.npix + (uint64_t)ntail * (chunks - 1) > 0xffffffffull) chunks = 1;
-        if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; }
+        if ((uint64_t)b.npix + (uint64_t)ntail * (std::max(chunks, chunks_mid) - 1) > 0xffffffffull) chunks = 1;
+        if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; nmid = 0; }
+        if (nmid == 0) chunks_mid = 1;
         b.chunks = chunks;
         b.ntail = ntail;
+        b.nmid = nmid;
+        b.chunks_mid = chunks_mid;
         b.nwhole = b.npix - ntail;
-        b.nunits = b.nwhole + ntail * chunks;
+        b.nunits = b.nwhole + nmid * chunks_mid + (ntail - nmid) * chunks;
         const uint32_t need = (b.nunits + paths_per_block - 1) / paths_per_block;
         if (blocks > need) blocks = need;
         if (ntail > 0) {

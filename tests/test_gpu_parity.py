@@ -175,6 +175,26 @@ def test_tail_split_units_bit_exact(oracle_mod, monkeypatch, tail, chunks, radiu
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("mid,fine_px,fine,radius", [("2", "0.0003", "5", 0.0), ("4", "0.0001", "9", 0.05),
+                                                    ("3", "0", "4", 0.0)])
+def test_two_level_split_units_bit_exact(oracle_mod, monkeypatch, mid, fine_px, fine, radius):
+    """Small shards split every pixel: all but the last pixels into `mid` chunks (longer units),
+    the last ~fine_px x resident lanes pixels into `fine` chunks (PT_WF_MID_CHUNKS /
+    PT_WF_FINE_PX / PT_WF_FINE_CHUNKS): the same image bits as the oracle."""
+    monkeypatch.setenv("PT_WF_MID_CHUNKS", mid)
+    monkeypatch.setenv("PT_WF_FINE_PX", fine_px)
+    monkeypatch.setenv("PT_WF_FINE_CHUNKS", fine)
+    s = load_scene("cornell_blob")
+    w, h, spp = 24, 16, 9
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=3)
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 0, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+
+
 @pytest.mark.parametrize("pool", ["128", "256"])
 @pytest.mark.parametrize("chunks,radius,flags,bounces", [
     ("1", 0.0, 0, 3), ("3", 0.0, 0, 3), ("1", 0.05, pt.PT_FLAG_COUNT, 3),
