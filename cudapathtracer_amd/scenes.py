@@ -129,15 +129,23 @@ def _blob_points(level, seed, amp=0.18):
     return v * disp[:, None], f
 
 
+def _write_atomic(path, text):
+    tmp = "%s.tmp%d" % (path, os.getpid())
+    with open(tmp, "w", newline="") as fh:
+        fh.write(text)
+    os.replace(tmp, path)
+
+
 def _write(dirpath, name, obj_text, mtl_text=None):
+    """MTL first, then the OBJ, each written to a private temp file and renamed into place: a
+    process that sees the OBJ (e.g. another rank of a multi-GPU bench sharing the scene cache)
+    sees both files complete."""
     models = os.path.join(dirpath, "models")
     os.makedirs(models, exist_ok=True)
     p = os.path.join(models, name + ".obj")
-    with open(p, "w", newline="") as fh:
-        fh.write(obj_text)
     if mtl_text is not None:
-        with open(os.path.join(models, name + ".mtl"), "w", newline="") as fh:
-            fh.write(mtl_text)
+        _write_atomic(os.path.join(models, name + ".mtl"), mtl_text)
+    _write_atomic(p, obj_text)
     return p
 
 
