@@ -5,11 +5,11 @@ Host surface (OBJ ingest, BVH build, camera, PPM) is C++ in csrc/host; the rende
 hand-written HIP in csrc/hip.  Python here is only orchestration over ctypes.
 """
 from ._lib import (PT_FLAG_COUNT, PT_FLAG_NO_DEAD_PATH_SKIP, PT_FLAG_NO_PRIMARY_CACHE,  # noqa: F401
-                   PT_FLAG_REFERENCE_TRAVERSAL, PT_FLAG_REFERENCE_BVH, PT_INTEGRATOR_HEAD, PT_INTEGRATOR_UNIDIR, PtError, LIB_PATH,
+                   PT_FLAG_REFERENCE_TRAVERSAL, PT_FLAG_REFERENCE_BVH, PT_INTEGRATOR_HEAD, PT_INTEGRATOR_UNIDIR, PtError, LIB_PATH, PT_E_INVALID,
                    PT_LIGHT_SPHERE)
 from . import api  # noqa: F401
-from .api import (Renderer, Scene, camera_ray, make_camera, morton_i_to_pxl, morton_pxl_to_i,  # noqa: F401
+from .api import (Group, Renderer, Scene, camera_ray, make_camera, morton_i_to_pxl, morton_pxl_to_i,  # noqa: F401
                   tonemap_u8, write_ppm, write_ppm_codes, write_pfm, read_pfm)
 
-__all__ = ["Scene", "Renderer", "make_camera", "camera_ray", "morton_pxl_to_i", "morton_i_to_pxl", "write_ppm", "write_ppm_codes", "write_pfm", "read_pfm",
+__all__ = ["Scene", "Renderer", "Group", "make_camera", "camera_ray", "morton_pxl_to_i", "morton_i_to_pxl", "write_ppm", "write_ppm_codes", "write_pfm", "read_pfm",
            "tonemap_u8", "PtError"]

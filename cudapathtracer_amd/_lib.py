@@ -22,7 +22,7 @@ PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
 PT_LIGHT_SPHERE = 0x80000000     # lights[] entry of an emissive sphere
-ABI_VERSION = 4                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
+ABI_VERSION = 5                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -70,7 +70,7 @@ class Stats(C.Structure):
                 ("rays_traced", C.c_uint64), ("rays_reference", C.c_uint64), ("rays_nominal", C.c_uint64),
                 ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("walk_lane_slots", C.c_uint64),
                 ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64),
-                ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64)]
+                ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64), ("spill_entries", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -104,10 +104,19 @@ SIGNATURES = {
     "pt_render_device": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.c_void_p,
                                    C.POINTER(Stats)]),
     "pt_trace": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "pt_trace_counts": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                  C.c_void_p, C.POINTER(C.c_uint64)]),
+    "pt_tri_counts": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "pt_tonemap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "pt_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pt_write_ppm_codes": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_write_pfm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "pt_group_create": (C.c_void_p, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_int)]),
+    "pt_group_size": (C.c_int, [C.c_void_p]),
+    "pt_render_group": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.POINTER(Stats)]),
+    "pt_group_destroy": (None, [C.c_void_p]),
+    "pt_render_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(Params), C.POINTER(Camera), C.c_void_p,
+                                  C.POINTER(Stats)]),
     "pt_destroy": (None, [C.c_void_p]),
 }
 

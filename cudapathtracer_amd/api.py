@@ -245,17 +245,79 @@ class Renderer:
         L.check(L.lib().pt_tonemap(self._h, img.ctypes.data, w, h, codes.ctypes.data))
         return codes
 
-    def trace(self, origins, directions, reference_bvh=False):
-        """The reference's trace() (kernel.cu:112-161) for a batch of rays: returns
-        (tri int32[n] original triangle index or -1, t float32[n] closestT, 1e5 on a miss)."""
+    def tri_counts(self):
+        """Per-triangle test counts (uint32[num_tris], original ids) of the last render with
+        PT_FLAG_COUNT -- the reference's test[] buffer (kernel.cu:133, :694-697)."""
+        n = int(self._scene_view.num_tris)
+        out = np.zeros(n, dtype=np.uint32)
+        L.check(L.lib().pt_tri_counts(self._h, out.ctypes.data, n))
+        return out
+
+    def trace_counts(self, origins, directions, reference_bvh=False):
+        """trace() plus diagnostics: returns (tri, t, tri_counts uint32[num_tris], spill_entries)."""
+        rays, n = self._rays(origins, directions)
+        tri = np.empty(n, dtype=np.int32)
+        t = np.empty(n, dtype=np.float32)
+        counts = np.zeros(int(self._scene_view.num_tris), dtype=np.uint32)
+        spills = C.c_uint64(0)
+        L.check(L.lib().pt_trace_counts(self._h, n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data,
+                                        L.PT_FLAG_REFERENCE_BVH if reference_bvh else 0, counts.ctypes.data,
+                                        C.byref(spills)))
+        return tri, t, counts, int(spills.value)
+
+    @staticmethod
+    def _rays(origins, directions):
         o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
         if o.shape != d.shape:
             raise ValueError("origins and directions differ in shape")
-        rays = np.ascontiguousarray(np.concatenate([o, d], axis=1))
-        n = len(rays)
+        return np.ascontiguousarray(np.concatenate([o, d], axis=1)), len(o)
+
+    def trace(self, origins, directions, reference_bvh=False):
+        """The reference's trace() (kernel.cu:112-161) for a batch of rays: returns
+        (tri int32[n] original triangle index or -1, t float32[n] closestT, 1e5 on a miss)."""
+        rays, n = self._rays(origins, directions)
         tri = np.empty(n, dtype=np.int32)
         t = np.empty(n, dtype=np.float32)
         L.check(L.lib().pt_trace(self._h, n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data,
                                  L.PT_FLAG_REFERENCE_BVH if reference_bvh else 0))
         return tri, t
+
+
+class Group:
+    """One process, N GPUs (pt_group_*): renderer i renders image-tile shard i of N, and one RCCL
+    reduce over xGMI sums the shards into the first renderer's device (bit-identical to one GPU).
+    The renderers must live on distinct devices and outlive the group."""
+
+    def __init__(self, renderers):
+        self._renderers = list(renderers)
+        arr = (C.c_void_p * len(self._renderers))(*[r._h for r in self._renderers])
+        err = C.c_int(0)
+        self._h = L.lib().pt_group_create(arr, len(self._renderers), C.byref(err))
+        if not self._h:
+            L.check(err.value if err.value != 0 else L.PT_E_HIP)
+
+    def close(self):
+        if self._h:
+            L.lib().pt_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self, cam, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0):
+        """Returns (image float32 (H, W, 3), summed stats dict)."""
+        p = Renderer.params(width, height, spp, bounces, integrator, seed, flags)
+        out = np.zeros((height, width, 3), dtype=np.float32)
+        st = L.Stats()
+        L.check(L.lib().pt_render_group(self._h, C.byref(p), C.byref(cam), out.ctypes.data, C.byref(st)))
+        return out, st.as_dict()

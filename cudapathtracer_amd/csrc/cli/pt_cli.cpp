@@ -9,14 +9,16 @@
 // --obj PATH[@ox,oy,oz[@scale[@flip]]]   loadOBJ(path, mtl dir, origin, scale, flipNormals)
 // --num-samples N                         the reference's NUM_SAMPLES (renders N-1 samples);
 //                                         --spp gives the sample count directly
-// --gpus N                                shard image tiles over devices 0..N-1 (one host thread
-//                                         and context per device; shards are disjoint, summed)
+// --gpus N                                shard image tiles over devices 0..N-1 (pt_render_multi:
+//                                         one context per device, one RCCL reduce of the shards)
+// --tri-counts out.csv                    per-triangle test counts (the reference's out.csv,
+//                                         kernel.cu:742-750); --reference-walk makes them the
+//                                         reference's own (its exact trace() sequence)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "pt/pt.h"
@@ -37,7 +39,8 @@ struct Obj {
             "usage: pt_cli --obj PATH[@ox,oy,oz[@scale[@flip]]] [--obj ...] [--mtl-dir DIR]\n"
             "              [--width W] [--height H] [--spp N | --num-samples N] [--bounces D]\n"
             "              [--integrator unidir|head] [--seed S] [--cam X,Y,Z] [--dist D] [--focal F]\n"
-            "              [--radius R] [--gpus N] [--out image.ppm] [--pfm image.pfm] [--quiet]\n");
+            "              [--radius R] [--gpus N] [--out image.ppm] [--pfm image.pfm] [--quiet]\n"
+            "              [--tri-counts out.csv [--reference-walk]]\n");
     exit(2);
 }
 
@@ -83,7 +86,8 @@ int main(int argc, char** argv)
     p.integrator = PT_INTEGRATOR_UNIDIR; p.seed = 1234; p.shard_index = 0; p.shard_count = 1;
     pt_camera cam{{0, 1, 3}, 1, 3, 0, 0, 0};                      // kernel.cu:642-648
     int gpus = 1;
-    bool quiet = false;
+    bool quiet = false, ref_walk = false;
+    std::string tri_csv;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> std::string {
@@ -111,11 +115,18 @@ int main(int argc, char** argv)
         else if (a == "--out") out = next();
         else if (a == "--pfm") pfm = next();
         else if (a == "--quiet") quiet = true;
+        else if (a == "--tri-counts") tri_csv = next();
+        else if (a == "--reference-walk") ref_walk = true;
         else if (a == "-h" || a == "--help") usage(nullptr);
         else usage(("unknown option " + a).c_str());
     }
     if (objs.empty()) usage("at least one --obj is required");
     if (gpus < 1) usage("--gpus must be >= 1");
+    if (!tri_csv.empty() && gpus != 1) usage("--tri-counts needs --gpus 1");
+    if (!tri_csv.empty()) p.flags |= PT_FLAG_COUNT;
+    // --reference-walk: the reference's own trace() sequence for every sample (its node order, the
+    // camera ray traced per sample, dead paths traced), so --tri-counts reproduces its out.csv
+    if (ref_walk) p.flags |= PT_FLAG_REFERENCE_TRAVERSAL | PT_FLAG_NO_PRIMARY_CACHE | PT_FLAG_NO_DEAD_PATH_SKIP;
     cam.pxl_width = p.width;
     cam.pxl_height = p.height;
 
@@ -142,30 +153,25 @@ int main(int argc, char** argv)
         ctx[g] = pt_create(&view, g, &err);
         if (!ctx[g]) return die("pt_create");
     }
-    std::vector<std::vector<float>> part(gpus, std::vector<float>(n));
-    std::vector<pt_stats> st(gpus);
-    std::vector<int> rc(gpus, PT_OK);
-    std::vector<std::thread> th;
-    const auto t1 = std::chrono::steady_clock::now();
-    for (int g = 0; g < gpus; ++g)
-        th.emplace_back([&, g]() {
-            pt_params q = p;
-            q.shard_index = g;
-            q.shard_count = gpus;
-            rc[g] = pt_render(ctx[g], &q, &cam, part[g].data(), &st[g]);
-        });
-    for (std::thread& t : th) t.join();
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
-    for (int g = 0; g < gpus; ++g)
-        if (rc[g] != PT_OK) return die("pt_render");
     std::vector<float> img(n, 0.0f);
-    uint64_t samples = 0, traced = 0, reference = 0, nominal = 0;
-    for (int g = 0; g < gpus; ++g) {
-        for (size_t k = 0; k < n; ++k) img[k] += part[g][k];   // disjoint shards: x + 0 = x
-        samples += st[g].samples;
-        traced += st[g].rays_traced;
-        reference += st[g].rays_reference;
-        nominal = st[g].rays_nominal;
+    pt_stats st{};
+    const auto t1 = std::chrono::steady_clock::now();
+    // one GPU: pt_render; N GPUs: image-tile shards on devices 0..N-1 summed by one RCCL reduce
+    const int rc = (gpus == 1) ? pt_render(ctx[0], &p, &cam, img.data(), &st)
+                               : pt_render_multi(ctx.data(), gpus, &p, &cam, img.data(), &st);
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    if (rc != PT_OK) return die("pt_render");
+    const uint64_t samples = st.samples, traced = st.rays_traced, reference = st.rays_reference;
+    const uint64_t nominal = st.rays_nominal;   // (summed over the shards)
+    if (!tri_csv.empty()) {
+        // kernel.cu:742-750: one "count,\n" line per entry of the reference's test[] buffer, which
+        // has bvh.size = numTris-1 entries (kernel.cu:696)
+        std::vector<uint32_t> counts(view.num_tris);
+        if (pt_tri_counts(ctx[0], counts.data(), view.num_tris) != PT_OK) return die("pt_tri_counts");
+        FILE* f = fopen(tri_csv.c_str(), "w");
+        if (!f) { fprintf(stderr, "pt_cli: cannot write %s\n", tri_csv.c_str()); return 1; }
+        for (uint32_t k = 0; k + 1 < view.num_tris; ++k) fprintf(f, "%u,\n", counts[k]);
+        fclose(f);
     }
     if (!quiet) {
         printf("%d GPU(s): %.3f s, %.1f Msamples/s, %.1f Mrays/s traced, %.1f Mrays/s reference-equivalent, "

@@ -244,10 +244,16 @@ __device__ __forceinline__ bool slab_ref(V3 o, V3 d, float lx, float ly, float l
 }
 
 struct Counters {
-    uint32_t nodes;        // node records fetched (64 B culled walk, 32 B reference walk)
-    uint32_t tris;         // triangle records tested (48 B)
-    uint32_t leaf_steps;   // walk steps that tested at least one triangle
-    uint32_t top = 0;      // BVH4 node visits served by the LDS copy of the tree's top
+    uint32_t nodes = 0;        // node records fetched (64 B culled walk, 32 B reference walk)
+    uint32_t tris = 0;         // triangle records tested (48 B)
+    uint32_t leaf_steps = 0;   // walk steps that tested at least one triangle
+    uint32_t top = 0;          // BVH4 node visits served by the LDS copy of the tree's top
+    uint32_t spills = 0;       // BVH4 stack entries written beyond the LDS ring (to the HBM spill column)
+    uint32_t* tri_counts = nullptr;   // per-triangle tests by ORIGINAL id (kernel.cu:133 test[k] += 1), or none
+    __device__ __forceinline__ void tri_tested(uint32_t id) const
+    {
+        if (tri_counts) atomicAdd(tri_counts + id, 1u);
+    }
 };
 
 // ------------------------------------------------------------------ exact division, cheaply
@@ -671,10 +677,14 @@ constexpr uint32_t kTopNodeBytes = 112;
 // 32000 B per block = 4 x 5120 B of rings + 160 B of counters + 101 x 112 B
 constexpr uint32_t kTopNodesMax = 101;
 
-__device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e)
+template <bool kCount>
+__device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e, Counters& cnt)
 {
     const int slot = (w.sp & (kRing - 1)) * 64;   // sp >= 0, kRing a power of two
-    if (w.sp >= kRing) S.spill()[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
+    if (w.sp >= kRing) {
+        S.spill()[(size_t)(w.sp - kRing) * S.stride] = S.ring[slot];
+        if (kCount) ++cnt.spills;
+    }
     S.ring[slot] = e;
     ++w.sp;
 }
@@ -741,6 +751,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     if (leaf) {
         const float t = tri_hit_pk(f2{o.x, o.y}, o.z, f2{d.x, d.y}, d.z, A, B, e2z);
         const uint32_t lslot = leaf4_slot(w);   // (recomputed here: one register less across the loads)
+        if (kCount) cnt.tri_tested(__float_as_uint(tris[lslot].c.y));
         // ties go to the lower reference DFS rank (the reference's first-visited); exact ties are
         // rare, so both ranks are read only then
         if (0.0f < t && (t < w.best_t ||
@@ -791,9 +802,9 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             top[128] = k1;
             w.sp += (int)v1 + (int)v2 + (int)v3;
         } else {
-            if (k3 != kNone) push4(w, S, k3);
-            if (k2 != kNone) push4(w, S, k2);
-            if (k1 != kNone) push4(w, S, k1);
+            if (k3 != kNone) push4<kCount>(w, S, k3, cnt);
+            if (k2 != kNone) push4<kCount>(w, S, k2, cnt);
+            if (k1 != kNone) push4<kCount>(w, S, k1, cnt);
         }
         w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
     }
@@ -819,7 +830,8 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
 // (entry k of this lane: node at gs[2k*stride], entry distance at gs[(2k+1)*stride]).
 __device__ __forceinline__ void trace_slow(V3 o, V3 d, const float* root, const DNode* __restrict__ nodes,
                                         const DTri* __restrict__ tris, uint32_t* gs, uint32_t stride,
-                                        float cull_rel, float cull_abs, int32_t* tri_out, float* t_out)
+                                        float cull_rel, float cull_abs, int32_t* tri_out, float* t_out,
+                                        uint32_t* tri_counts = nullptr)
 {
     const V3 y = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float best_t = kMaxFloat;
@@ -844,6 +856,7 @@ __device__ __forceinline__ void trace_slow(V3 o, V3 d, const float* root, const 
                 const DTri* tr = tris + (r ^ kLeaf);
                 uint32_t id;
                 const float t = tri_hit<false>(o, d, tr, &id);
+                if (tri_counts) atomicAdd(tri_counts + id, 1u);
                 const uint32_t rank = __float_as_uint(tr->c.z);
                 if (0.0f < t && (t < best_t || (t == best_t && rank < best_rank))) { best_t = t; best_rank = rank; best_id = id; }
             } else {
@@ -902,7 +915,7 @@ __device__ __forceinline__ Hit trace_reference(V3 o, V3 d, const RNode* __restri
             uint32_t id;
             const float t = tri_t_rec(o, d, tris + k, &id);
             if (0.0f < t && t < closest) { closest = t; best = (int32_t)k; }
-            if (kCount) ++cnt.tris;
+            if (kCount) { ++cnt.tris; cnt.tri_tested(k); }   // kernel.cu:133 (tris is in original order)
             --i;
         } else {
             const RNode* nd = nodes + e;
@@ -959,7 +972,7 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
             const uint32_t slot = D.x ^ kLeaf;
             uint32_t id;
             const float t = tri_t_rec(o, d, tris + slot, &id);
-            if (kCount) ++cnt.tris;
+            if (kCount) { ++cnt.tris; cnt.tri_tested(id); }
             if (0.0f < t && (t < best_t || (t == best_t && slot < best_slot))) { best_t = t; best_slot = slot; best_id = id; }
         } else {
             const bool hit = slab_ref(o, d, A.x, A.y, A.z, A.w, B.x, B.y, &ti, &to);
@@ -970,7 +983,7 @@ __device__ __forceinline__ Hit trace_culled(V3 o, V3 d, const float* root, const
             const uint32_t slot = D.y ^ kLeaf;
             uint32_t id;
             const float t = tri_t_rec(o, d, tris + slot, &id);
-            if (kCount) ++cnt.tris;
+            if (kCount) { ++cnt.tris; cnt.tri_tested(id); }
             if (0.0f < t && (t < best_t || (t == best_t && slot < best_slot))) { best_t = t; best_slot = slot; best_id = id; }
             // a leaf found now may already beat the left box: re-check it
             h0 = h0 && !(t0 > best_t * cull_rel);

@@ -61,9 +61,7 @@ struct Args {
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
     uint32_t* spill;                // LDS-stack overflow, entry k of lane g at spill[(k-kRing)*stride + g]
     uint32_t spill_stride;
-    uint32_t cold_stride;           // records of the cold array (lanes, or paths of the pool kernel)
-    float4* pray;                   // pool kernel: path g's ray and pending hit at pray[2g], pray[2g+1]:
-                                    // (o.x, o.y, o.z, d.x), (d.y, d.z, hit slot / id, hit t)
+    uint32_t cold_stride;           // records of the cold array (one per resident lane)
     float acc_root[6];
     uint32_t* cold;                 // per-lane shading state of the wavefront kernel (ColdRec)
     const uint32_t* pix_states;     // per work unit u, word k at [k*nunits + u] (kUnitWords, init_pixel_states)
@@ -81,6 +79,7 @@ struct Args {
     uint32_t num_spheres;
     uint32_t num_tris;
     uint32_t sphere_mat_base;       // material of sphere i = mats[sphere_mat_base + i]
+    uint32_t* tri_counts;           // PT_FLAG_COUNT: per-triangle test counts by original id (kernel.cu:133)
 };
 
 __device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
@@ -472,9 +471,7 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
     tr.a = &a;
     tr.stack = lds_stack;
     tr.lane = lane;
-    tr.cnt.nodes = 0;
-    tr.cnt.tris = 0;
-    tr.cnt.leaf_steps = 0;
+    if (kCount) tr.cnt.tri_counts = a.tri_counts;
     tr.traced = 0;
     tr.reference = 0;
     unsigned long long samples = 0;
@@ -554,8 +551,7 @@ enum : int {
     CW_PX = 28, CW_PY, CW_MTRI, CW_MT,        // cell 7: pixel, primary memo (tri, t)
     CW_CD = 32,                               // cell 8: camera ray direction of a pinhole unit (CF_CAMC) ...
     CW_Q = 35,                                //         ... and a split unit's tail slot (per-sample buffer row)
-    CW_PST = 36,                              // cell 9: path-pool kernel: path state while queued for shading
-    kColdWords = 40
+    kColdWords = 36
 };
 // CF_ACC0: the sample's accumulator is 0 (not yet written: the record's acc words are stale)
 enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64,
@@ -855,7 +851,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             wave_count(lcnt + 3, lane);
             SEC(SEC_SLOW);
             trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs,
-                       &htri, &ht);
+                       &htri, &ht, kCount ? a.tri_counts : nullptr);
         }
         state = ST_SHADE;
         if (a.num_spheres && !(fl & CF_MEMO)) apply_spheres(a, ro, rd, &htri, &ht);
@@ -1106,9 +1102,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     __syncthreads();
     const int lane = threadIdx.x & 63;
     Counters cnt;
-    cnt.nodes = 0;
-    cnt.tris = 0;
-    cnt.leaf_steps = 0;
+    if (kCount) cnt.tri_counts = a.tri_counts;
     if (kCount && threadIdx.x == 0) atomicMin(a.counters + 20, (unsigned long long)wall_clock64());   // first start
     uint32_t walk_slots = 0, shade_slots = 0;   // counting variant: SIMD lane-slot usage
     uint32_t trace_slots = 0, steps = 0;        // counting variant: lanes tracing per iteration; steps of this walk
@@ -1206,7 +1200,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             atomicAdd(a.counters + 24, 1ull);
         }
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
-        const unsigned long long c13 = wave_sum(cnt.top);
+        const unsigned long long c13 = wave_sum(cnt.top), c25 = wave_sum(cnt.spills);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
         const unsigned long long c11 = wave_sum(trace_slots);
         if (lane == 0) {
@@ -1214,6 +1208,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7); atomicAdd(a.counters + 11, c11);
             atomicAdd(a.counters + 12, (unsigned long long)start_wait);
             atomicAdd(a.counters + 13, c13);
+            atomicAdd(a.counters + 25, c25);
             for (int k = 0; k < 6; ++k) atomicAdd(a.counters + 14 + k, (unsigned long long)itc[k]);
         }
     }
@@ -1225,220 +1220,6 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
     }
     if (kCount && threadIdx.x < kSections + kHist) {   // section counts, then the histogram
-        const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
-        if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
-    }
-}
-
-// ------------------------------------------------------------------ path-pool kernel
-// The same state machine with kPaths > 64 paths per wave, so that a lane whose ray is done can
-// start another at once.  Each wave owns kPaths path records (ColdRec, CW_RO.. for the ray and
-// pending hit) and two LDS queues of path slots: TQ (ray ready to trace) and SQ (hit ready to
-// shade, or a path to refill).  Walk phase: lanes without a ray take the next TQ entry; a
-// finished walk stores the hit and queues the path on SQ; the phase ends when TQ is empty and
-// wf_threshold lanes are free (or nothing is tracing).  Shade phase: the free lanes shade SQ
-// paths, round after round, until SQ is empty, queueing each path's next ray on TQ.  Per path
-// the arithmetic and RNG draws are exactly those of render_unidir_wf (shade_lane is shared);
-// only which lane runs a path, and when, changes.
-// number of lanes below this one set in m (v_mbcnt)
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-template <int kPaths>
-__device__ __forceinline__ ColdRec path_rec(const Args& a, uint32_t g)
-{
-    return ColdRec{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
-                   g * 16u, a.cold_stride * 16u};
-}
-
-template <bool kCount, int kMinWaves, int kPaths>
-__global__ __launch_bounds__(256, kMinWaves) void render_unidir_pool(Args a)
-{
-    static_assert(kPaths >= 64 && kPaths <= 256 && (kPaths & (kPaths - 1)) == 0, "pool size: 64..256, power of 2");
-    extern __shared__ uint32_t lds_wf[];
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform (SGPR)
-    const int lane = threadIdx.x & 63;
-    // LDS: 4 waves' rings, then per wave TQ and SQ (kPaths u16 each), then the block counters.
-    // A TQ entry is slot | octant << 8: the ray's direction signs pick the near planes of the
-    // first node fetch before the ray itself arrives.
-    uint16_t* const TQ = reinterpret_cast<uint16_t*>(lds_wf + 4 * kWaveLdsWords) + wv * 2 * kPaths;
-    uint16_t* const SQ = TQ + kPaths;
-    unsigned long long* lcnt = reinterpret_cast<unsigned long long*>(lds_wf + 4 * kWaveLdsWords + 4 * kPaths);
-    if (threadIdx.x < 4 + kSections / 2) lcnt[threadIdx.x] = 0ull;   // 4 counters + the section counts
-    Counters cnt;
-    cnt.nodes = 0;
-    cnt.tris = 0;
-    cnt.leaf_steps = 0;
-    uint32_t walk_slots = 0, shade_slots = 0;
-    unsigned long long walk_clk = 0, shade_clk = 0;
-
-    Stack4 S;
-    S.ring = lds_wf + wv * kWaveLdsWords + lane;
-    S.stride = a.spill_stride;
-    const uint32_t lane_off = (blockIdx.x * blockDim.x + threadIdx.x) * 4u;
-    S.spill_base = a.spill;
-    S.lane_off = &lane_off;
-    S.off_mask = ~0u;
-    const uint32_t path0 = (blockIdx.x * 4u + (uint32_t)wv) * (uint32_t)kPaths;
-
-    // every path starts idle, queued for shading (which gives it a unit)
-    for (int j = lane; j < kPaths; j += 64) {
-        SQ[j] = (uint16_t)j;
-        path_rec<kPaths>(a, path0 + (uint32_t)j).st(CW_PST, ST_IDLE);
-    }
-    __syncthreads();
-    // wave-uniform queue state (ring offsets mod kPaths)
-    uint32_t tq_head = 0, tq_n = 0, sq_head = 0, sq_n = kPaths;
-
-    uint32_t cur = kNone;   // path slot this lane is tracing
-    bool fresh = false;     // its ray is still to be fetched and set up (first step)
-    uint32_t state = ST_IDLE;
-    V3 ro = v3(0, 0, 0), rd = v3(0, 0, 1);
-    W4 w;
-    int32_t htri = -1;
-    float ht = kMaxFloat;
-
-    for (;;) {
-        // ---------------------------------------------------------------- walk
-        unsigned long long clk0 = 0;
-        if (kCount) clk0 = clock64();
-        for (;;) {
-            uint64_t idle = __ballot(cur == kNone);
-            if (tq_n > 0 && idle != 0ull) {
-                const uint32_t take = min((uint32_t)__popcll(idle), tq_n);
-                const uint32_t rank = lane_rank(idle);
-                if (cur == kNone && rank < take) {
-                    // the ray is fetched and set up inside the first step, with the root fetch in
-                    // flight (the root test passed when the ray was queued)
-                    const uint32_t e = TQ[(tq_head + rank) & (kPaths - 1)];
-                    cur = e & 255u;
-                    walk4_reset(w);
-                    w.nx = (e & 0x100u) ? 48u : 0u;   // == walk4_setup's choice (sign of d = sign of 1/d)
-                    w.ny = (e & 0x200u) ? 64u : 16u;
-                    w.nz = (e & 0x400u) ? 80u : 32u;
-                    fresh = true;
-                }
-                tq_head = (tq_head + take) & (kPaths - 1);
-                tq_n -= take;
-                idle = __ballot(cur == kNone);
-            }
-            if (idle == ~0ull) break;
-            if (tq_n == 0 && sq_n > 0 && (uint32_t)__popcll(idle) >= a.wf_threshold) break;
-            if (kCount) ++walk_slots;
-            bool fin = false;
-            if (cur != kNone) {
-                const auto setup = [&](W4& ww) {
-                    if (fresh) {
-                        const float4* pr = a.pray + 2 * (size_t)(path0 + cur);
-                        const float4 r0 = pr[0], r1 = pr[1];
-                        ro = v3(r0.x, r0.y, r0.z);
-                        rd = v3(r0.w, r1.x, r1.y);
-                        walk4_setup(ww, ro, rd);
-                        fresh = false;
-                    }
-                };
-                const bool more = walk4_step<kCount>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
-                                                     a.node_mask, cnt, setup);
-                if (!more) {
-                    // the winner's check against the reference BVH runs when the path is shaded
-                    float2* hp = reinterpret_cast<float2*>(a.pray + 2 * (size_t)(path0 + cur) + 1) + 1;
-                    *hp = make_float2(__uint_as_float(w.best_slot), w.best_t);
-                    path_rec<kPaths>(a, path0 + cur).st(CW_PST, (w.best_slot == kNone) ? ST_SHADE : ST_CHECK);
-                    fin = true;
-                }
-            }
-            const uint64_t done = __ballot(fin);
-            if (done) {
-                if (fin) {
-                    SQ[(sq_head + sq_n + lane_rank(done)) & (kPaths - 1)] = (uint16_t)cur;
-                    cur = kNone;
-                }
-                sq_n += (uint32_t)__popcll(done);
-            }
-        }
-        if (kCount) {
-            const unsigned long long c = clock64();
-            walk_clk += c - clk0;
-            clk0 = c;
-        }
-        if (sq_n == 0) break;   // nothing tracing, nothing queued: every path is done
-
-        // ---------------------------------------------------------------- shade rounds
-        for (bool first = true; sq_n > 0; first = false) {
-            const uint64_t avail = __ballot(cur == kNone);
-            if (avail == 0ull) break;   // (wf_threshold 0: every lane may still be tracing)
-            // only full rounds after the first: a remainder waits for the next shade phase
-            // (when nothing is tracing and nothing is queued to trace, it must go now)
-            if (!first && sq_n < (uint32_t)__popcll(avail) && (tq_n > 0 || avail != ~0ull)) break;
-            const uint32_t take = min((uint32_t)__popcll(avail), sq_n);
-            const uint32_t rank = lane_rank(avail);
-            uint32_t js = kNone;
-            if (cur == kNone && rank < take) js = SQ[(sq_head + rank) & (kPaths - 1)];
-            sq_head = (sq_head + take) & (kPaths - 1);
-            sq_n -= take;
-            if (kCount) ++shade_slots;
-            bool to_t = false, to_s = false;
-            if (js != kNone) {
-                const ColdRec P = path_rec<kPaths>(a, path0 + js);
-                float4* pr = a.pray + 2 * (size_t)(path0 + js);
-                state = P.ld(CW_PST);
-                {   // (garbage for a path that was never given a unit: shade_lane then only refills)
-                    const float4 r0 = pr[0], r1 = pr[1];
-                    ro = v3(r0.x, r0.y, r0.z);
-                    rd = v3(r0.w, r1.x, r1.y);
-                    htri = (int32_t)__float_as_uint(r1.z);
-                    ht = r1.w;
-                }
-                shade_lane<kCount>(a, P, lane, state, ro, rd, htri, ht, w, S, lcnt);
-                if (state != ST_DONE) {
-                    // ST_TRACE: the next ray; otherwise shading is pending right after a refill
-                    // (memo hit, root miss, slow ray) and the hit travels with it
-                    pr[0] = make_float4(ro.x, ro.y, ro.z, rd.x);
-                    pr[1] = make_float4(rd.y, rd.z, __uint_as_float((uint32_t)htri), ht);
-                    if (state == ST_TRACE) {
-                        to_t = true;
-                    } else {
-                        P.st(CW_PST, state);
-                        to_s = true;
-                    }
-                }
-            }
-            const uint64_t bt = __ballot(to_t), bs = __ballot(to_s);
-            if (to_t) {
-                const uint32_t oct = (__float_as_uint(rd.x) >> 31) | ((__float_as_uint(rd.y) >> 31) << 1) |
-                                     ((__float_as_uint(rd.z) >> 31) << 2);
-                TQ[(tq_head + tq_n + lane_rank(bt)) & (kPaths - 1)] = (uint16_t)(js | (oct << 8));
-            }
-            if (to_s) SQ[(sq_head + sq_n + lane_rank(bs)) & (kPaths - 1)] = (uint16_t)js;
-            tq_n += (uint32_t)__popcll(bt);
-            sq_n += (uint32_t)__popcll(bs);
-        }
-        if (kCount) shade_clk += clock64() - clk0;
-    }
-    if (kCount) {
-        if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
-        if (lane == 0) {   // wave exit times (wall clock): last, and the sum for the mean
-            const unsigned long long t = wall_clock64();
-            atomicMax(a.counters + 22, t);
-            atomicAdd(a.counters + 23, t);
-            atomicAdd(a.counters + 24, 1ull);
-        }
-        const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
-        const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
-        if (lane == 0) {
-            atomicAdd(a.counters + 2, c2); atomicAdd(a.counters + 3, c3v); atomicAdd(a.counters + 5, c5);
-            atomicAdd(a.counters + 6, c6); atomicAdd(a.counters + 7, c7);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicAdd(a.counters + 0, lcnt[0]);
-        atomicAdd(a.counters + 1, lcnt[1]);
-        atomicAdd(a.counters + 4, lcnt[2]);
-        if (lcnt[3]) atomicAdd(a.counters + 8, lcnt[3]);
-    }
-    if (kCount && threadIdx.x < kSections) {
         const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
         if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
     }
@@ -1477,14 +1258,14 @@ __global__ __launch_bounds__(256) void tonemap_codes(const float* __restrict__ r
 // pt_trace: the reference's trace() (kernel.cu:112-161) for a batch of rays, one lane per ray,
 // on the same walk the wavefront kernel uses (BVH4 + winner check + exact slow path), or on the
 // reference BVH with the reference's own stack walk (kRef).
-template <bool kRef>
+template <bool kRef, bool kCount>
 __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restrict__ rays, uint32_t n,
                                                   int32_t* __restrict__ tri_out, float* __restrict__ t_out)
 {
     extern __shared__ uint32_t lds_tr[];
     const int lane = threadIdx.x & 63;
     Counters cnt;
-    cnt.nodes = cnt.tris = cnt.leaf_steps = 0;
+    if (kCount) cnt.tri_counts = a.tri_counts;
     Stack4 S;
     // per wave: the reference walk's stack (stack_words) or the BVH4 rings (kWaveLdsWords)
     uint32_t* const wave_lds = lds_tr + (threadIdx.x >> 6) * a.stack_words;
@@ -1502,14 +1283,15 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
         if (a.num_tris == 0) {
             // spheres only
         } else if (kRef) {
-            const Hit h = trace_reference<false>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
+            const Hit h = trace_reference<kCount>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
             htri = h.tri; ht = h.t;
         } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
-            trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs, &htri, &ht);
+            trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs, &htri, &ht,
+                       cnt.tri_counts);
         } else {
             W4 w;
             if (walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
-                while (walk4_step<false>(w, o, d, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs, a.node_mask, cnt)) {
+                while (walk4_step<kCount>(w, o, d, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs, a.node_mask, cnt)) {
                 }
                 ht = w.best_t;
                 bool ok = true;
@@ -1521,13 +1303,17 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
                 if (!ok) {
                     atomicAdd(a.counters + 8, 1ull);
                     trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs,
-                               &htri, &ht);
+                               &htri, &ht, cnt.tri_counts);
                 }
             }
         }
         if (a.num_spheres) apply_spheres(a, o, d, &htri, &ht);
         tri_out[r] = htri;
         t_out[r] = ht;
+    }
+    if (kCount) {
+        const unsigned long long sp = wave_sum(cnt.spills);
+        if (lane == 0 && sp) atomicAdd(a.counters + 25, sp);
     }
 }
 
@@ -1637,12 +1423,9 @@ struct pt_ctx {
                                     // -1 = automatic, 0 or 1 = one split for all)
     double wf_fine_px = 0.5;        // ... the last pixels per resident lane (PT_WF_FINE_PX)
     int wf_fine_chunks = 0;         // ... and their chunks (PT_WF_FINE_CHUNKS; 0 = the automatic count)
-    float4* pray = nullptr;           // pool kernel: per-path ray + pending hit
-    size_t pray_words = 0;
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
     uint32_t wf_top = kTopNodesMax; // BVH4 nodes staged in each block's LDS (PT_WF_TOP; 0 = none)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
-    int wf_pool = 0;                // paths per wave of the path-pool kernel (128 / 256), 0 = one per lane (PT_WF_POOL)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
@@ -1662,7 +1445,10 @@ struct pt_ctx {
     float acc_root[6];
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
+    uint32_t* tri_counts = nullptr;   // PT_FLAG_COUNT: per-triangle test counts (num_tris entries, >= 1)
 };
+
+int pt::ctx_device(const pt_ctx* c) { return c->device; }
 
 // Per-lane HBM words the walks may need: the BVH4 ring's overflow (at most 3 pushes per level)
 // and trace_slow's full stack on the reference BVH.
@@ -1850,10 +1636,6 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_FINE_CHUNKS")) c->wf_fine_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
-        if (const char* e = getenv("PT_WF_POOL")) {
-            const int v = atoi(e);
-            c->wf_pool = (v == 128 || v == 256) ? v : 0;
-        }
     }
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
     std::vector<DNode4> an;
@@ -2020,7 +1802,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
-        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar))) {
+        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) ||
+        (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u)))) {
         pt_destroy(c);
         return bail(rc);
     }
@@ -2043,7 +1826,7 @@ void pt_destroy(pt_ctx* c)
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
-                    c->tone_thr, c->spheres, c->pray};
+                    c->tone_thr, c->spheres, c->tri_counts};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -2112,6 +1895,10 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
     HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
+    if (count) {   // per-triangle test counts of this render (read back with pt_tri_counts)
+        HIP_TRY(hipMemsetAsync(c->tri_counts, 0, (size_t)std::max<uint32_t>(c->num_tris, 1u) * 4, stream));
+        a.tri_counts = c->tri_counts;
+    }
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
     const uint32_t waves_per_cu = 16;
@@ -2133,8 +1920,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         // pixel slots are split into sample chunks, so the final units are short.
         // A shard with too few pixels to keep every resident lane busy is split entirely.
         b.npix = a.ntiles_shard * 64u;
-        const uint32_t pool = (uint32_t)c->wf_pool;   // (pool kernels: 5 waves per SIMD)
-        const uint32_t paths_per_block = pool ? 4u * pool : 256u;
+        const uint32_t paths_per_block = 256u;
         const uint64_t lanes = (uint64_t)blocks * paths_per_block;   // concurrently running paths
         uint32_t chunks = 1, ntail = 0, nmid = 0, chunks_mid = 1;
         if (c->wf_tail_npix >= 0) {   // (tests: an explicit tail)
@@ -2165,6 +1951,26 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         // (measured on C3 shards: whole pixels down to ~3 per lane; below that ~16 units per lane:
         // 1/8 shard 20 chunks, 1/4 shard 10)
         if (chunks > (uint32_t)p->spp) chunks = (uint32_t)p->spp;
+        // Split pixels keep their per-sample radiance (lbuf: 24 B per sample), so the split is
+        // capped at a memory budget (PT_LBUF_BUDGET_MB; default a quarter of the device memory
+        // free now, plus what lbuf already holds): beyond it the first tail slots become whole-pixel
+        // units instead (the split only shortens the kernel's tail; results are identical).
+        if (ntail > 0 && chunks > 1) {
+            uint64_t budget;
+            if (const char* e = getenv("PT_LBUF_BUDGET_MB")) {
+                budget = (uint64_t)std::max(0.0, atof(e)) * (1ull << 20);
+            } else {
+                size_t fr = 0, tot = 0;
+                HIP_TRY(hipMemGetInfo(&fr, &tot));
+                budget = ((uint64_t)fr + (uint64_t)c->lbuf_words * sizeof(double)) / 4;
+            }
+            const uint64_t cap = budget / ((uint64_t)p->spp * 3 * sizeof(double));
+            if (ntail > cap) {
+                const uint32_t drop = ntail - (uint32_t)cap;   // taken from the front: mid grade first
+                nmid = nmid > drop ? nmid - drop : 0;
+                ntail = (uint32_t)cap;
+            }
+        }
         if ((uint64_t)b.npix + (uint64_t)ntail * (std::max(chunks, chunks_mid) - 1) > 0xffffffffull) chunks = 1;
         if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; nmid = 0; }
         if (nmid == 0) chunks_mid = 1;
@@ -2204,17 +2010,6 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.spill_stride = blocks * 256;
         b.cold_stride = blocks * paths_per_block;
         b.cold = c->spill + per_lane * (size_t)b.spill_stride;
-        if (pool) {
-            const size_t pw = (size_t)b.cold_stride * 8;   // 2 float4 per path
-            if (c->pray_words < pw) {
-                if (c->pray) (void)hipFree(c->pray);
-                c->pray = nullptr;
-                c->pray_words = 0;
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pray), pw * 4));
-                c->pray_words = pw;
-            }
-            b.pray = c->pray;
-        }
         const size_t sw = (size_t)kUnitWords * b.nunits;
         if (c->pix_states_words < sw) {
             if (c->pix_states) (void)hipFree(c->pix_states);
@@ -2225,12 +2020,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         }
         b.pix_states = c->pix_states;
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
-        const size_t lds_pool = (size_t)kWaveLdsWords * 4 * 4 + 4 * 4 * (size_t)pool + 4 * sizeof(unsigned long long) + kSections * 4;
-        if (pool == 128 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
-        else if (pool == 256 && count) hipLaunchKernelGGL((render_unidir_pool<true, 5, 256>), dim3(blocks), dim3(256), lds_pool, stream, b);
-        else if (pool == 128) hipLaunchKernelGGL((render_unidir_pool<false, 5, 128>), dim3(blocks), dim3(256), lds_pool, stream, b);
-        else if (pool == 256) hipLaunchKernelGGL((render_unidir_pool<false, 5, 256>), dim3(blocks), dim3(256), lds_pool, stream, b);
-        else if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
@@ -2287,6 +2077,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         st->accel_fallbacks = cnt[8];
         st->walk_cycles = cnt[9];
         st->shade_cycles = cnt[10];
+        st->spill_entries = cnt[25];
         const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
         st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
     }
@@ -2335,6 +2126,23 @@ static int ensure_spill(pt_ctx* c, size_t words)
 
 extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags)
 {
+    return pt_trace_counts(c, n, rays, tri_out, t_out, flags, nullptr, nullptr);
+}
+
+extern "C" int pt_tri_counts(pt_ctx* c, uint32_t* counts, uint32_t n)
+{
+    pt::clear_error();
+    if (!c || !counts) return pt::fail(PT_E_INVALID, "pt_tri_counts: null argument");
+    if (n != c->num_tris) return pt::fail(PT_E_INVALID, "pt_tri_counts: n = %u, the scene has %u triangles", n, c->num_tris);
+    if (n == 0) return PT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy(counts, c->tri_counts, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags,
+                               uint32_t* tri_counts, uint64_t* spill_entries)
+{
     pt::clear_error();
     if (!c) return pt::fail(PT_E_INVALID, "pt_trace: null context");
     if (n == 0) return PT_OK;
@@ -2374,14 +2182,30 @@ extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_o
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_tri), (size_t)n * 4));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_t), (size_t)n * 4));
         HIP_TRY(hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemset(c->counters, 0, 16 * sizeof(unsigned long long)));
-        if (flags & PT_FLAG_REFERENCE_BVH)
-            hipLaunchKernelGGL((trace_rays<true>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
-        else
-            hipLaunchKernelGGL((trace_rays<false>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        HIP_TRY(hipMemset(c->counters, 0, 64 * sizeof(unsigned long long)));
+        const bool count = tri_counts != nullptr || spill_entries != nullptr;
+        if (tri_counts && c->num_tris > 0) {
+            HIP_TRY(hipMemset(c->tri_counts, 0, (size_t)c->num_tris * 4));
+            a.tri_counts = c->tri_counts;
+        }
+        const bool ref = (flags & PT_FLAG_REFERENCE_BVH) != 0;
+        if (ref && count) hipLaunchKernelGGL((trace_rays<true, true>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        else if (ref) hipLaunchKernelGGL((trace_rays<true, false>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        else if (count) hipLaunchKernelGGL((trace_rays<false, true>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
+        else hipLaunchKernelGGL((trace_rays<false, false>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpy(tri_out, d_tri, (size_t)n * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(t_out, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
+        if (tri_counts && c->num_tris > 0) {   // added to the caller's counts (kernel.cu:133 accumulates)
+            std::vector<uint32_t> h(c->num_tris);
+            HIP_TRY(hipMemcpy(h.data(), c->tri_counts, (size_t)c->num_tris * 4, hipMemcpyDeviceToHost));
+            for (uint32_t k = 0; k < c->num_tris; ++k) tri_counts[k] += h[k];
+        }
+        if (spill_entries) {
+            unsigned long long v = 0;
+            HIP_TRY(hipMemcpy(&v, c->counters + 25, sizeof(v), hipMemcpyDeviceToHost));
+            *spill_entries = v;
+        }
         return PT_OK;
     };
     rc = run();

@@ -21,6 +21,9 @@ namespace pt {
 int fail(int code, const char* fmt, ...);
 void clear_error();
 
+// The HIP device ordinal a render context lives on (pt_render.hip; used by pt_multi.cpp).
+int ctx_device(const pt_ctx* c);
+
 // ---- OBJ/MTL ingest with tinyobj 0.9.13 semantics (tiny_obj_loader.cc) ------------------
 // Only what loadOBJ (modelLoader.h:125-210) consumes is kept: positions, per-triangle
 // indices, per-triangle material ids, material diffuse/emission.  Vertex dedupe keys still

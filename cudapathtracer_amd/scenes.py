@@ -470,3 +470,37 @@ def add_cornell_spheres(scene, spheres=CORNELL_SPHERES):
     for pos, rad, diffuse, emission in spheres:
         scene.add_sphere(pos, rad, diffuse, emission)
     return scene
+
+
+# ----------------------------------------------------------------------------- stack stress (C5 row)
+# "Splinters": long thin triangles crossing the whole box in random directions.  Every BVH box
+# then spans most of the volume and a ray enters nearly all of them, so a BVH4 walk pushes ~3
+# entries per level on its way down -- deeper than the 16-entry per-lane LDS ring, i.e. the
+# HBM spill tier (the reference's fixed stack[64], kernel.cu:114, + depth guard :627-631) runs.
+SPLINTERS_MTL = """# splinters (stack-depth stress scene) materials
+newmtl splinter
+Kd 0.6 0.55 0.5
+newmtl light
+Kd 0.8 0.8 0.8
+Ke 15 15 15
+"""
+
+
+def write_splinters(dirpath, n=1024, seed=5, name="splinters"):
+    rng = np.random.default_rng(seed)
+    lo, hi = np.array([-1.0, 0.05, -1.0]), np.array([1.0, 1.95, 1.0])
+    a = rng.uniform(lo, hi, (n, 3))
+    b = rng.uniform(lo, hi, (n, 3))
+    far = np.linalg.norm(b - a, axis=1) < 1.2            # keep them long: re-draw the end point
+    b[far] = lo + hi - a[far]
+    c = a + rng.normal(scale=0.02, size=(n, 3))           # thin: a sliver along a -> b
+    w = _ObjWriter()
+    w.raw("# splinters: %d long thin triangles in random directions (stack-depth stress)" % n)
+    w.raw("mtllib %s.mtl" % name)
+    w.raw("usemtl splinter")
+    base = w.verts(np.stack([a, b, c], axis=1).reshape(-1, 3))
+    w.faces(np.arange(3 * n).reshape(n, 3), base)
+    w.raw("usemtl light")
+    lb = w.verts([(-0.3, 1.99, -0.3), (0.3, 1.99, -0.3), (0.3, 1.99, 0.3), (-0.3, 1.99, 0.3)])
+    w.faces([(0, 2, 1), (0, 3, 2)], lb)                   # facing -y (the NEE light normal, kernel.cu:503)
+    return _write(dirpath, name, w.text(), SPLINTERS_MTL)

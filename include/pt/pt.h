@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4
+#define PT_ABI_VERSION 5
 
 /* ---- status codes */
 #define PT_OK 0
@@ -144,7 +144,8 @@ typedef struct pt_ctx pt_ctx;
                                              the exact node/triangle sequence of kernel.cu:112-161 */
 #define PT_FLAG_NO_DEAD_PATH_SKIP 0x2u    /* trace every bounce even after the path weight is 0   */
 #define PT_FLAG_NO_PRIMARY_CACHE 0x4u     /* re-trace the (sample-invariant) camera ray per sample  */
-#define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant)     */
+#define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant), incl.
+                                             the per-triangle counts of kernel.cu:133 (pt_tri_counts) */
 #define PT_FLAG_REFERENCE_BVH 0x10u       /* culled walk on the reference BVH only (no SAH BVH)     */
 
 typedef struct {
@@ -166,7 +167,9 @@ typedef struct {
     uint64_t rays_reference;   /* trace() calls the reference integrator performs for the same
                                   samples (differs from rays_traced by the primary-ray cache and
                                   the dead-path skip)                                             */
-    uint64_t rays_nominal;     /* W*H*spp*(bounces+1): the kernel.cu:757 formula, in 64-bit       */
+    uint64_t rays_nominal;     /* pixels*spp*(bounces+1) over THIS render's pixels (its shard; the
+                                  whole image for pt_render_group): the kernel.cu:757 formula, in
+                                  64-bit                                                          */
     uint64_t node_tests;       /* node records fetched (PT_FLAG_COUNT only)                       */
     uint64_t tri_tests;        /* triangle records tested (PT_FLAG_COUNT only)                    */
     uint64_t walk_lane_slots;  /* PT_FLAG_COUNT, wavefront kernel: 64 x BVH-walk iterations; with
@@ -179,6 +182,9 @@ typedef struct {
     uint64_t walk_cycles;      /* PT_FLAG_COUNT, wavefront kernel: wave-clock cycles spent in walk
                                   phases, summed over waves                                     */
     uint64_t shade_cycles;     /* same for shading (+ refill) phases                              */
+    uint64_t spill_entries;    /* PT_FLAG_COUNT, BVH4 walk: stack entries pushed beyond the 16-entry
+                                  per-lane LDS ring into the lane's HBM spill column (the reference's
+                                  fixed stack[64] of kernel.cu:114 has no such tier)              */
 } pt_stats;
 
 /* Host-only diagnostic: builds the render path's private acceleration structure for `scene`
@@ -206,6 +212,22 @@ int pt_render_device(pt_ctx* ctx, const pt_params* params, const pt_camera* cam,
  * reference's own stack walk on its BVH.  Bit-identical to the reference for both.  Blocking. */
 int pt_trace(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags);
 
+/* trace() as above, plus diagnostics (either may be NULL):
+ *   tri_counts[num_tris]: every triangle test of the walk ADDED to tri_counts[original id] --
+ *     the reference's test[k] += 1 (kernel.cu:133); with PT_FLAG_REFERENCE_BVH exactly the
+ *     reference's counts for these rays, otherwise the tests the render path's walk performed;
+ *   spill_entries: BVH4 stack entries pushed past the per-lane LDS ring into HBM. */
+int pt_trace_counts(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags,
+                    uint32_t* tri_counts, uint64_t* spill_entries);
+
+/* Per-triangle test counts (n = num_tris entries, by original triangle id) of the ctx's last
+ * pt_render / pt_render_device with PT_FLAG_COUNT: the reference's bvhIntersection buffer
+ * (kernel.cu:694-697, written to out.csv at :742-750).  With PT_FLAG_REFERENCE_TRAVERSAL |
+ * PT_FLAG_NO_PRIMARY_CACHE | PT_FLAG_NO_DEAD_PATH_SKIP the render performs exactly the reference's
+ * trace() calls, so these are the reference's counts (without its racy increments and with the
+ * last triangle's slot, which the reference's numTris-1 buffer lacks). */
+int pt_tri_counts(pt_ctx* ctx, uint32_t* counts, uint32_t n);
+
 /* Output step on the GPU (kernel.cu:763-778, color.h:59-71): codes = pt_tonemap_u8(rgb) per
  * channel, identical to the host function (threshold table bisected with the host's libm at
  * pt_create).  _device: device pointers on `stream`, blocking; negative inputs (which the
@@ -213,6 +235,25 @@ int pt_trace(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out, float
  * pt_tonemap: host buffers, negatives handled. */
 int pt_tonemap_device(pt_ctx* ctx, const float* d_rgb, int width, int height, int32_t* d_codes, void* stream);
 int pt_tonemap(pt_ctx* ctx, const float* rgb, int width, int height, int32_t* codes);
+
+/* ----------------------------------------------------------- one process, N GPUs
+ * A group of contexts on distinct devices with one RCCL communicator per device
+ * (ncclCommInitAll).  pt_render_group renders shard i of N on context i -- image tiles dealt
+ * round-robin, tile t -> context t % N (params' shard fields are ignored) -- concurrently, one
+ * host thread and HIP stream per device, each into a zero-filled fp32 framebuffer, then ONE
+ * ncclReduce(sum, root = ctxs[0]'s device) over xGMI and one copy of the image to out_rgb:
+ * bit-identical to a single-GPU pt_render (every pixel is its shard's value plus zeros).  Stats
+ * are summed over the shards; `seconds` is the job's wall time (renders + reduce + copy).
+ * Replaces the reference's launch loop (kernel.cu:709-736) and its D2H copy (:760).
+ * The group does not own the contexts; destroy it before them. */
+typedef struct pt_group pt_group;
+pt_group* pt_group_create(pt_ctx* const* ctxs, int n, int* err);
+int pt_group_size(const pt_group* group);
+int pt_render_group(pt_group* group, const pt_params* params, const pt_camera* cam, float* out_rgb, pt_stats* stats);
+void pt_group_destroy(pt_group* group);
+/* create + render + destroy */
+int pt_render_multi(pt_ctx* const* ctxs, int n, const pt_params* params, const pt_camera* cam, float* out_rgb,
+                    pt_stats* stats);
 
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(void);

@@ -50,7 +50,8 @@ class OScene(C.Structure):
 
 
 class OCounters(C.Structure):
-    _fields_ = [("traces", C.c_uint64), ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64)]
+    _fields_ = [("traces", C.c_uint64), ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("tri_counts", C.c_void_p)]
 
 
 _lib = None
@@ -72,6 +73,8 @@ def lib():
         h.or_sincos.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         h.or_trace_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         h.or_trace_batch.restype = C.c_int
+        h.or_trace_batch_counts.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        h.or_trace_batch_counts.restype = C.c_int
         h.or_tri_intersect.argtypes = [OVec3, OVec3, C.c_void_p, C.c_void_p]
         h.or_tri_intersect.restype = C.c_float
         h.or_ray_aabb.argtypes = [OVec3, OVec3, OVec3, OVec3]
@@ -122,13 +125,18 @@ def camera(pos, dist_from_film, focal_length, radius, width, height):
 
 
 def render(scene: OracleScene, cam: OCamera, width, height, spp, bounces=3, integrator=0, seed=1234, pixels=None,
-           threads=0):
-    """f64 mean image (H, W, 3); pixels = iterable of y*W+x (default: all).  Returns (img, counters)."""
+           threads=0, tri_counts=None):
+    """f64 mean image (H, W, 3); pixels = iterable of y*W+x (default: all).  Returns (img, counters).
+    tri_counts: optional uint32[num_tris] array the per-triangle test counts are added to
+    (kernel.cu:133 test[k] += 1)."""
     if pixels is None:
         pixels = np.arange(width * height, dtype=np.uint32)
     pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
     out = np.zeros((height, width, 3), dtype=np.float64)
     cnt = OCounters()
+    if tri_counts is not None:
+        assert tri_counts.dtype == np.uint32 and tri_counts.flags.c_contiguous and len(tri_counts) == scene.c.num_tris
+        cnt.tri_counts = tri_counts.ctypes.data
     rc = lib().or_render(C.byref(scene.c), C.byref(cam), width, height, spp, bounces, integrator, seed,
                          pixels.ctypes.data, len(pixels), threads, out.ctypes.data, C.byref(cnt))
     if rc != 0:
@@ -145,15 +153,19 @@ def trace(scene: OracleScene, o, d):
     return tri.value, t.value
 
 
-def trace_batch(scene: OracleScene, origins, directions):
-    """or_trace over many rays (OpenMP): returns (tri int32[n], t float32[n])."""
+def trace_batch(scene: OracleScene, origins, directions, tri_counts=None):
+    """or_trace over many rays (OpenMP): returns (tri int32[n], t float32[n]); tri_counts (optional
+    uint32[num_tris]) accumulates the per-triangle test counts of kernel.cu:133."""
     o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
     d = np.ascontiguousarray(directions, dtype=np.float32).reshape(-1, 3)
     rays = np.ascontiguousarray(np.concatenate([o, d], axis=1))
     n = len(rays)
     tri = np.empty(n, dtype=np.int32)
     t = np.empty(n, dtype=np.float32)
-    if lib().or_trace_batch(C.byref(scene.c), n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data) != 0:
+    if tri_counts is not None:
+        assert tri_counts.dtype == np.uint32 and tri_counts.flags.c_contiguous and len(tri_counts) == scene.c.num_tris
+    cp = tri_counts.ctypes.data if tri_counts is not None else None
+    if lib().or_trace_batch_counts(C.byref(scene.c), n, rays.ctypes.data, tri.ctypes.data, t.ctypes.data, cp) != 0:
         raise RuntimeError("stack overflow")
     return tri, t
 

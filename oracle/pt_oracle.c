@@ -345,6 +345,7 @@ int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float
             float t = or_tri_intersect(o, dir, sc->verts, sc->tris + k);
             if (0.0f < t && t < closest) { closest = t; tri = (int32_t)k; }
             ++tt;
+            if (cnt && cnt->tri_counts) __atomic_fetch_add(cnt->tri_counts + k, 1u, __ATOMIC_RELAXED);  /* :133 */
             --i;
         } else {
             const or_node* nd = sc->bvh + e;
@@ -371,11 +372,18 @@ int or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri_out, float
 
 int or_trace_batch(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t)
 {
+    return or_trace_batch_counts(sc, n, rays, tri, t, NULL);
+}
+
+int or_trace_batch_counts(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t,
+                          uint32_t* tri_counts)
+{
     int bad = 0;
 #pragma omp parallel for schedule(dynamic, 256) reduction(+ : bad)
     for (long r = 0; r < (long)n; ++r) {
         or_counters cnt;
         memset(&cnt, 0, sizeof(cnt));
+        cnt.tri_counts = tri_counts;
         const float* q = rays + 6 * r;
         or_vec3 o = {q[0], q[1], q[2]}, d = {q[3], q[4], q[5]};
         bad += or_trace(sc, o, d, tri + r, t + r, &cnt) != 0;
@@ -652,7 +660,7 @@ int or_render(const or_scene* sc, const or_camera* cam, int width, int height,
         uint32_t idx = or_morton_pxl_to_i(px, py);
         or_xorwow rng;
         or_xorwow_init(seed, idx, &rng);
-        or_counters c = {0, 0, 0};
+        or_counters c = {0, 0, 0, cnt ? cnt->tri_counts : NULL};
         double mean[3] = {0, 0, 0};
         int lens_draws = (idx == 0) || (cam->radius != 0.0f);
         for (int n = 1; n <= spp; ++n) {

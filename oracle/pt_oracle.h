@@ -66,6 +66,7 @@ typedef struct {                                                   /* modelLoade
 
 typedef struct {
     uint64_t traces, node_tests, tri_tests;
+    uint32_t* tri_counts;   /* optional (NULL = off): per-triangle test counts, kernel.cu:133 test[k] += 1 */
 } or_counters;
 
 /* ---- RNG (kernel.cu:527-533 curand_init(1234, idx, 0); kernel.cu:56-59 curand_uniform) */
@@ -90,6 +91,9 @@ int      or_trace(const or_scene* sc, or_vec3 o, or_vec3 dir, int32_t* tri, floa
 float    or_sphere_t(or_vec3 o, or_vec3 d, const or_sphere* s);   /* MAX_FLOAT on a miss */
 /* or_trace over rays[6n] = {o.xyz, d.xyz} (OpenMP); returns the number of stack overflows. */
 int      or_trace_batch(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t);
+/* The same, also adding every triangle test to tri_counts[num_tris] (kernel.cu:133). */
+int      or_trace_batch_counts(const or_scene* sc, uint32_t n, const float* rays, int32_t* tri, float* t,
+                               uint32_t* tri_counts);
 
 /* ---- integrators */
 /* kernel.cu:417-515 radianceAlongSingleStep2 (integrator 0) */

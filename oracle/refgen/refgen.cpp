@@ -5,8 +5,12 @@
 // command line / below: CUDA's function-space qualifiers __host__/__device__ are
 // defined empty (a host compile), and min/max/abs are brought in from <algorithm>/<cmath>
 // as the reference's nvcc build got them from CUDA's math headers.  No header,
-// library or generated file is substituted.  kernel.cu itself is NOT built (it needs
-// cuda_runtime.h, cuRAND, NVML, windows.h and the broken triple.h -- see DESIGN.md).
+// library or generated file is substituted.  kernel.cu as a whole is NOT built (it needs
+// cuda_runtime.h, cuRAND, NVML, windows.h and the broken triple.h -- see DESIGN.md); its
+// trace() (kernel.cu:107-161: struct triIntersection + trace) needs none of those, so
+// oracle/Makefile extracts exactly that span from /root/reference/kernel.cu at build time into
+// oracle/_ref/ref_trace.inc (git-ignored, never committed) and it is #included below verbatim,
+// with MAX_BVH_DEPTH = 64 as kernel.cu:35 defines it.
 //
 // Built by oracle/Makefile into oracle/_ref/refgen (git-ignored).  Driven by
 // tools/make_golden.py, which writes tests/golden/*.
@@ -18,6 +22,11 @@
 //   refgen cam   <in.bin> <out.bin>   in: {cam 32 B} + n x {idx u32, u1 f32, u2 f32}; out: n x {o[3], d[3]} f32
 //   refgen morton <out.bin> <n>       out: n x {x u16, y u16, back u32} for idx 0..n-1
 //   refgen tone  <in.bin> <out.bin>   in: n x 3 f64 ; out: n x 3 i32 = (int)(gammaCorrect(normalized(c), 1/2.2)*255)
+//   refgen trace <rays.bin> <out.bin> <counts.bin> <obj> <ox> <oy> <oz> <scale> <flip> [<obj> ...]  (cwd as for scene)
+//                in: n x {o[3], d[3]} f32 ; out: n x {triIndex i32, t f32} from kernel.cu:112 trace() on the
+//                scene's buildBVH() array; counts: numTris x u32, the trace()'s test[] increments summed
+//                over all rays (kernel.cu:133; sized numTris here -- the reference's buffer has
+//                bvh.size = numTris-1 entries, kernel.cu:696, so its last increment lands out of bounds)
 #include <cstdint>
 #include <cmath>
 #include <cstdio>
@@ -35,6 +44,10 @@ using std::abs;
 #include "/root/reference/modelLoader.h"
 #include "/root/reference/BVH.h"
 #include "/root/reference/camera.h"
+#ifdef REFGEN_TRACE
+#define MAX_BVH_DEPTH 64   // kernel.cu:35
+#include REFGEN_TRACE      // kernel.cu:107-161, extracted verbatim by oracle/Makefile
+#endif
 
 static std::vector<char> slurp(const char* path)
 {
@@ -164,6 +177,39 @@ int main(int argc, char** argv)
         spit(argv[3], out.data(), out.size() * 4);
         return 0;
     }
+#ifdef REFGEN_TRACE
+    if (cmd == "trace") {
+        std::vector<char> in = slurp(argv[2]);
+        const size_t n = in.size() / 24;
+        for (int a = 5; a + 5 < argc; a += 6) {
+            vec3 origin((float)atof(argv[a + 1]), (float)atof(argv[a + 2]), (float)atof(argv[a + 3]));
+            loadOBJ(argv[a], origin, (float)atof(argv[a + 4]), atoi(argv[a + 5]) != 0);   // modelLoader.h:125
+        }
+        if (tris.size() < 2) { fprintf(stderr, "refgen trace: need >= 2 triangles\n"); return 2; }
+        BVH_array bvh = buildBVH();                                                      // BVH.h:443
+        if (bvh.depth >= MAX_BVH_DEPTH) { fprintf(stderr, "refgen trace: BVH depth too big\n"); return 2; }   // kernel.cu:627
+        sceneDesc scene;                                                                 // kernel.cu:664-689
+        scene.numVerts = (uint32_t)verts.size(); scene.verts = verts.data();
+        scene.numTris = (uint32_t)tris.size(); scene.tris = tris.data();
+        scene.numMats = (uint32_t)mats.size(); scene.mats = mats.data();
+        scene.numLights = (uint32_t)lights.size(); scene.lights = (uint32_t*)lights.data();
+        scene.totalLightArea = totalLightArea;
+        std::vector<uint32_t> test(tris.size(), 0u);
+        std::vector<char> out(n * 8);
+        const float* p = (const float*)in.data();
+        for (size_t i = 0; i < n; ++i) {
+            ray r;
+            r.o = vec3(p[6 * i], p[6 * i + 1], p[6 * i + 2]);
+            r.dir = vec3(p[6 * i + 3], p[6 * i + 4], p[6 * i + 5]);
+            triIntersection h = trace(r, scene, bvh, test.data());                          // kernel.cu:112
+            memcpy(&out[8 * i], &h.triIndex, 4);
+            memcpy(&out[8 * i + 4], &h.t, 4);
+        }
+        spit(argv[3], out.data(), out.size());
+        spit(argv[4], test.data(), test.size() * 4);
+        return 0;
+    }
+#endif
     fprintf(stderr, "refgen: unknown command %s\n", cmd.c_str());
     return 2;
 }

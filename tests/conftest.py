@@ -49,6 +49,19 @@ def load_scene(name, build_bvh=True):
 
 
 @pytest.fixture(scope="session")
+def standin_scene(tmp_path_factory):
+    """The ~262K-triangle stand-in (cudapathtracer_amd.scenes), loaded once per session."""
+    import cudapathtracer_amd as pt
+    from cudapathtracer_amd import scenes
+    d = tmp_path_factory.mktemp("standin")
+    p = scenes.write_sponza_standin(str(d))
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    s.build_bvh()
+    return s
+
+
+@pytest.fixture(scope="session")
 def scene_cache():
     return {}
 

@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_error_channel():
     L = _lib.lib()
-    assert L.pt_abi_version() == 4
+    assert L.pt_abi_version() == 5
     rc = L.pt_render(None, None, None, None, None)
     assert rc == _lib.PT_E_INVALID
     assert b"null" in L.pt_last_error()
@@ -75,3 +75,20 @@ def test_no_cpu_fallback_in_product():
                 assert "import oracle" not in txt and "pt_oracle" not in txt and "liboracle" not in txt, f
     out = subprocess.check_output(["ldd", _lib.LIB_PATH]).decode()
     assert "oracle" not in out
+
+
+def test_group_entry_points_reject_bad_arguments():
+    """pt_group_* / pt_render_multi (one process, N GPUs, RCCL reduce) validate before touching a
+    device: no contexts, a null context, null buffers."""
+    L = _lib.lib()
+    err = C.c_int(0)
+    assert not L.pt_group_create(None, 0, C.byref(err)) and err.value == _lib.PT_E_INVALID
+    arr = (C.c_void_p * 2)(None, None)
+    assert not L.pt_group_create(arr, 2, C.byref(err)) and err.value == _lib.PT_E_INVALID
+    assert b"null" in L.pt_last_error()
+    assert L.pt_render_group(None, None, None, None, None) == _lib.PT_E_INVALID
+    assert L.pt_render_multi(None, 0, None, None, None, None) == _lib.PT_E_INVALID
+    assert L.pt_group_size(None) == 0
+    L.pt_group_destroy(None)
+    assert L.pt_tri_counts(None, None, 0) == _lib.PT_E_INVALID
+    assert L.pt_trace_counts(None, 1, None, None, None, 0, None, None) == _lib.PT_E_INVALID

@@ -55,3 +55,30 @@ def test_cli_render_matches_oracle(tmp_path):
     exp = str(tmp_path / "expected.ppm")
     pt.write_ppm(exp, ref)
     assert open(ppm, "rb").read() == open(exp, "rb").read()
+
+
+def test_cli_tri_counts_needs_one_gpu(tmp_path):
+    r = _run(_obj_args("cornell") + ["--tri-counts", str(tmp_path / "out.csv"), "--gpus", "2"])
+    assert r.returncode == 2 and "--tri-counts" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_tri_counts_csv_matches_reference_walk(tmp_path):
+    """--tri-counts out.csv --reference-walk: the reference's out.csv (kernel.cu:742-750, one
+    "count," line per entry of its numTris-1 test[] buffer) from the reference's own trace()
+    sequence -- equal to the oracle's per-triangle counts (trace() pinned to the reference)."""
+    import oracle
+    w, h, spp = 16, 16, 2
+    csv = str(tmp_path / "out.csv")
+    r = _run(_obj_args("cornell_blob") + ["--width", str(w), "--height", str(h), "--spp", str(spp), "--quiet",
+                                          "--out", str(tmp_path / "i.ppm"), "--tri-counts", csv, "--reference-walk"])
+    assert r.returncode == 0, r.stderr
+    lines = open(csv).read().split("\n")
+    assert lines[-1] == "" and all(x.endswith(",") for x in lines[:-1])
+    got = np.array([int(x[:-1]) for x in lines[:-1]], dtype=np.uint32)
+    s = load_scene("cornell_blob")
+    osc = oracle.OracleScene(s.arrays())
+    counts = np.zeros(len(osc.tris), dtype=np.uint32)
+    oracle.render(osc, oracle.camera((0.0, 1.0, 3.0), 1.0, 3.0, 0.0, w, h), w, h, spp, 3, 0, 1234, tri_counts=counts)
+    assert len(got) == len(counts) - 1
+    assert np.array_equal(got, counts[:-1])

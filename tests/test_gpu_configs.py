@@ -5,7 +5,8 @@ non-negative, sample counts, shard disjointness).
 
 C2  Cornell mesh 1024x1024, 64 spp, depth 8
 C3  262K-triangle stand-in 1920x1080, 256 spp, depth 3 (the bench workload)
-C4  same at 1024 spp, one GPU's shard of 8 (sample-chunk work units at scale)
+C4  same at 1024 spp: all 8 shards of the 8-GPU partition rendered in turn and summed ==
+    the full frame (sample-chunk work units at scale)
 C5  stand-in 3840x2160, 4096 spp, depth 16
 """
 import os
@@ -58,7 +59,7 @@ def test_c2_cornell_1024_64spp_depth8():
         img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 64, bounces=8)
     assert np.isfinite(img).all() and (img >= 0).all()
     assert st["samples"] == w * h * 64
-    _check(s, img, cam_kw, w, h, 64, 8, _spread(w, h, 48, 1))
+    _check(s, img, cam_kw, w, h, 64, 8, _spread(w, h, 4096, 1))
 
 
 def test_c3_standin_1080p_256spp(standin):
@@ -68,22 +69,47 @@ def test_c3_standin_1080p_256spp(standin):
     img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 256, bounces=3)
     assert np.isfinite(img).all() and (img >= 0).all()
     assert st["samples"] == w * h * 256
-    _check(s, img, cam_kw, w, h, 256, 3, _spread(w, h, 24, 2))
+    _check(s, img, cam_kw, w, h, 256, 3, _spread(w, h, 4096, 2))
 
 
-def test_c4_standin_1080p_1024spp_shard_of_8(standin):
+def test_c4_standin_1080p_1024spp_eight_shards_sum_to_full_frame(standin):
+    """C4 as the 8-GPU job partitions it, on one GPU: all 8 image-tile shards rendered in turn
+    (each with its split-pixel work units), disjoint, summed (what the RCCL reduce computes) --
+    bit-identical to the full-frame render, whose spread of pixels equals the oracle."""
     s, r = standin
-    w, h = 1920, 1080
+    w, h, spp = 1920, 1080, 1024
     cam_kw = scenes.SPONZA_STANDIN_CAMERA
-    img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 1024, bounces=3,
-                       shard_index=3, shard_count=8)
-    mine = shard.shard_pixels(w, h, 3, 8)
-    mask = np.zeros(w * h, dtype=bool)
-    mask[mine] = True
-    assert np.all(img.reshape(-1, 3)[~mask] == 0)
-    assert st["samples"] == len(mine) * 1024
-    rng = np.random.default_rng(3)
-    _check(s, img, cam_kw, w, h, 1024, 3, np.unique(rng.choice(mine, 12, replace=False)).astype(np.uint32))
+    cam = pt.make_camera(width=w, height=h, **cam_kw)
+    full, st = r.render(cam, w, h, spp, bounces=3)
+    assert st["samples"] == w * h * spp
+    acc = np.zeros_like(full)
+    seen = np.zeros(w * h, dtype=np.int32)
+    samples = 0
+    for k in range(8):
+        part, sk = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=8)
+        mine = shard.shard_pixels(w, h, k, 8)
+        mask = np.zeros(w * h, dtype=bool)
+        mask[mine] = True
+        assert np.all(part.reshape(-1, 3)[~mask] == 0)
+        seen[mine] += 1
+        samples += sk["samples"]
+        acc += part
+    assert np.all(seen == 1) and samples == w * h * spp
+    assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+    _check(s, full, cam_kw, w, h, spp, 3, _spread(w, h, 2048, 3))
+
+
+def test_c3_fast_walk_equals_reference_walk_full_frame(standin):
+    """Every pixel of C3: the measured wavefront kernel (BVH4 walk, culling, winner check, memo,
+    dead-path skip, split units) equals the tile kernel walking the reference BVH in the
+    reference's own node order (PT_FLAG_REFERENCE_TRAVERSAL), bit for bit."""
+    s, r = standin
+    w, h, spp = 1920, 1080, 256
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    a, sa = r.render(cam, w, h, spp, bounces=3)
+    b, sb = r.render(cam, w, h, spp, bounces=3, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa["rays_reference"] == sb["rays_reference"] and sa["samples"] == sb["samples"]
 
 
 def test_c5_standin_4k_4096spp_depth16(standin):
@@ -93,7 +119,7 @@ def test_c5_standin_4k_4096spp_depth16(standin):
     img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, 4096, bounces=16)
     assert np.isfinite(img).all() and (img >= 0).all()
     assert st["samples"] == w * h * 4096
-    _check(s, img, cam_kw, w, h, 4096, 16, _spread(w, h, 6, 4))
+    _check(s, img, cam_kw, w, h, 4096, 16, _spread(w, h, 512, 4))
 
 
 @pytest.mark.parametrize("top", ["0", "17", "64"])

@@ -195,34 +195,6 @@ def test_two_level_split_units_bit_exact(oracle_mod, monkeypatch, mid, fine_px, 
     assert st["rays_reference"] == cnt["traces"]
 
 
-@pytest.mark.parametrize("pool", ["128", "256"])
-@pytest.mark.parametrize("chunks,radius,flags,bounces", [
-    ("1", 0.0, 0, 3), ("3", 0.0, 0, 3), ("1", 0.05, pt.PT_FLAG_COUNT, 3),
-    ("5", 0.0, pt.PT_FLAG_NO_DEAD_PATH_SKIP | pt.PT_FLAG_NO_PRIMARY_CACHE, 8), ("1", 0.0, 0, 16)])
-def test_path_pool_kernel_bit_exact(oracle_mod, monkeypatch, pool, chunks, radius, flags, bounces):
-    """The path-pool kernel (kPaths paths per wave, LDS trace/shade queues; PT_WF_POOL): the same
-    image bits, sample count and reference trace count as the oracle, with whole-pixel and
-    sample-chunk units, the lens, the counting variant and both skip modes off."""
-    monkeypatch.setenv("PT_WF_POOL", pool)
-    monkeypatch.setenv("PT_WF_CHUNKS", chunks)
-    s = load_scene("cornell_blob")
-    w, h, spp = 40, 24, 5
-    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
-    with pt.Renderer(s, 0) as r:
-        img, st = r.render(cam, w, h, spp, bounces=bounces, flags=flags)
-        parts = np.zeros_like(img)
-        for k in range(2):
-            part, _ = r.render(cam, w, h, spp, bounces=bounces, flags=flags, shard_index=k, shard_count=2)
-            parts += part
-    ref, cnt = _oracle(oracle_mod, s, w, h, spp, bounces, 0, radius=radius)
-    assert _bits_equal(img, ref) == 0
-    assert _bits_equal(parts, img.astype(np.float64)) == 0
-    assert st["samples"] == w * h * spp
-    assert st["rays_reference"] == cnt["traces"]
-    if flags & pt.PT_FLAG_COUNT:
-        assert st["node_tests"] > 0 and 0 < st["walk_lane_slots"]
-
-
 def test_rmse_and_properties_larger(oracle_mod, cb):
     """North-star tolerance on a subset of a larger render (oracle only on the subset)."""
     s, r = cb
@@ -278,3 +250,73 @@ def test_gpu_output_step_equals_host_tonemap(cb, tmp_path):
                     dtype=np.float32)
     e = np.resize(edge, (1, 4, 3))
     assert np.array_equal(r.tonemap(e), np.vectorize(pt.tonemap_u8)(e.astype(np.float64)))
+
+
+@pytest.mark.parametrize("integ", [0, 1])
+def test_per_triangle_counts_match_reference(oracle_mod, cb, integ):
+    """The reference's test[] buffer (kernel.cu:133, :694-697): with the reference traversal and
+    both shortcuts off the render performs exactly the reference's trace() calls, so the
+    per-triangle test counts equal the oracle's (whose trace is pinned to the reference's own
+    trace(), tests/test_oracle.py); the default fast path reports the tests it performed."""
+    s, r = cb
+    w, h, spp = 24, 16, 3
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    flags = (pt.PT_FLAG_REFERENCE_TRAVERSAL | pt.PT_FLAG_NO_PRIMARY_CACHE | pt.PT_FLAG_NO_DEAD_PATH_SKIP |
+             pt.PT_FLAG_COUNT)
+    img, st = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=flags)
+    counts = r.tri_counts()
+    osc = oracle_mod.OracleScene(s.arrays())
+    ocam = oracle_mod.camera(CAM["pos"], CAM["dist_from_film"], CAM["focal_length"], 0.0, w, h)
+    ocounts = np.zeros(len(osc.tris), dtype=np.uint32)
+    ref, cnt = oracle_mod.render(osc, ocam, w, h, spp, 3, integ, 1234, tri_counts=ocounts)
+    assert _bits_equal(img, ref) == 0
+    assert np.array_equal(counts, ocounts)
+    assert int(counts.sum()) == st["tri_tests"] == cnt["tri_tests"]
+    # the fast path's own counts: fewer tests, same image
+    img2, st2 = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=pt.PT_FLAG_COUNT)
+    fast = r.tri_counts()
+    assert _bits_equal(img2, ref) == 0
+    assert 0 < int(fast.sum()) < int(counts.sum())
+    assert int(fast.sum()) >= st2["tri_tests"]
+
+
+@pytest.mark.parametrize("budget", ["0", "0.002"])
+def test_split_buffer_budget_fallback_bit_exact(oracle_mod, monkeypatch, budget):
+    """Split pixels keep per-sample radiance (24 B per sample); over the memory budget
+    (PT_LBUF_BUDGET_MB) the split shrinks -- to nothing at 0, to a few slots at 2 KB -- and the
+    shards still sum to the oracle's image bit for bit."""
+    monkeypatch.setenv("PT_LBUF_BUDGET_MB", budget)
+    s = load_scene("cornell_blob")
+    w, h, spp = 64, 48, 6
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    with pt.Renderer(s, 0) as r:
+        full, st = r.render(cam, w, h, spp, bounces=3)
+        parts = np.zeros_like(full)
+        for k in range(4):
+            part, _ = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=4)
+            parts += part
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 0)
+    assert _bits_equal(full, ref) == 0
+    assert _bits_equal(parts, ref) == 0
+    assert st["rays_reference"] == cnt["traces"]
+
+
+def test_group_render_one_device_equals_render(cb):
+    """pt_render_group (RCCL reduce of the image-tile shards) on the box's one device: a
+    1-communicator group, bit-identical to pt_render, stats summed; a second context on the same
+    device is refused (one context per device)."""
+    s, r = cb
+    w, h, spp = 40, 24, 4
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    ref, st = r.render(cam, w, h, spp, bounces=3)
+    with pt.Group([r]) as g:
+        img, gst = g.render(cam, w, h, spp, bounces=3)
+        img2, _ = g.render(cam, w, h, spp, bounces=3)   # buffers and communicator reused
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(img2.view(np.uint32), ref.view(np.uint32))
+    assert gst["samples"] == st["samples"] == w * h * spp
+    assert gst["rays_nominal"] == st["rays_nominal"] == w * h * spp * 4
+    with pt.Renderer(s, 0) as r2:
+        with pytest.raises(pt.PtError) as e:
+            pt.Group([r, r2])
+        assert e.value.code == pt.PT_E_INVALID

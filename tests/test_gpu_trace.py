@@ -10,60 +10,13 @@ import os
 import numpy as np
 import pytest
 
-from conftest import load_scene
+from conftest import golden, load_scene
+from raysets import bounce_rays, ray_sets
 
 import cudapathtracer_amd as pt
 from cudapathtracer_amd import scenes
 
 pytestmark = pytest.mark.gpu
-
-
-def _unit(v):
-    return (v / np.linalg.norm(v, axis=1)[:, None]).astype(np.float32)
-
-
-def ray_sets(arrays, n, seed):
-    """Dict of named (origins, directions) float32 arrays over the scene's bounds."""
-    rng = np.random.default_rng(seed)
-    v = arrays["verts"]
-    P = np.stack([v["x"], v["y"], v["z"]], axis=1).astype(np.float64)
-    lo, hi = P.min(0), P.max(0)
-    ext = hi - lo
-    out = {}
-    o = rng.uniform(lo + 0.05 * ext, hi - 0.05 * ext, (n, 3))
-    out["interior"] = (o.astype(np.float32), _unit(rng.normal(size=(n, 3))))
-    d = rng.normal(size=(n, 3))
-    axis = rng.integers(0, 3, n)
-    zero = rng.integers(0, 3, n)
-    d[np.arange(n), zero] = 0.0                     # one zero component
-    d[: n // 3] = 0.0
-    d[np.arange(n // 3), axis[: n // 3]] = rng.choice([-1.0, 1.0], n // 3)   # axis-parallel
-    out["axis"] = (o.astype(np.float32), _unit(d))
-    # origins on vertices and on their coordinate planes
-    pick = P[rng.integers(0, len(P), n)]
-    o2 = pick.copy()
-    o2[n // 2:, 0] = rng.uniform(lo[0], hi[0], n - n // 2)
-    out["vertex_planes"] = (o2.astype(np.float32), _unit(rng.normal(size=(n, 3))))
-    # tiny components: outside the Markstein preconditions (exact slow path)
-    d3 = rng.normal(size=(n, 3))
-    d3[:, 1] = rng.choice([1e-31, -1e-36, 3e-39, 1e-20], n)
-    out["tiny"] = (o.astype(np.float32), _unit(d3))
-    # from outside: aimed at the scene
-    c = 0.5 * (lo + hi)
-    far = c + _unit(rng.normal(size=(n, 3))) * (2.0 * np.linalg.norm(ext) + 1.0)
-    tgt = rng.uniform(lo, hi, (n, 3))
-    out["outside"] = (far.astype(np.float32), _unit(tgt - far))
-    return out
-
-
-def bounce_rays(arrays, o, d, tri, t, seed):
-    """Rays leaving the surfaces hit by (o, d) the way the integrator builds them
-    (kernel.cu:455-470: pos = o + d * (float)(t - 0.001))."""
-    rng = np.random.default_rng(seed)
-    hit = tri >= 0
-    tt = (t[hit].astype(np.float64) - 0.001).astype(np.float32)
-    pos = (o[hit] + d[hit] * tt[:, None]).astype(np.float32)
-    return pos, _unit(rng.normal(size=(len(pos), 3)))
 
 
 def _check(r, osc, oracle_mod, o, d, name):
@@ -111,3 +64,60 @@ def test_trace_bit_exact_standin(tmp_path):
         _check(r, osc, oracle_mod, bo, bd, "bounce")
         for k, (o2, d2) in ray_sets(a, 5000, 11).items():
             _check(r, osc, oracle_mod, o2, d2, k)
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_blob", "quirks", "standin"])
+def test_trace_matches_reference_trace_goldens(name, request):
+    """Both walks against the reference's OWN trace() (kernel.cu:107-161 compiled from
+    /root/reference by oracle/Makefile; tests/golden/kat_trace_*.npz): (triIndex, closestT)
+    bit for bit, and the reference walk's per-triangle test counts (kernel.cu:133) exactly."""
+    g = golden("kat_trace_%s.npz" % name)
+    s = request.getfixturevalue("standin_scene") if name == "standin" else load_scene(name)
+    o, d = g["rays"][:, :3], g["rays"][:, 3:]
+    with pt.Renderer(s, 0) as r:
+        for ref in (False, True):
+            tri, t = r.trace(o, d, reference_bvh=ref)
+            bad = np.nonzero((tri != g["tri"]) | (t.view(np.uint32) != g["t"].view(np.uint32)))[0]
+            assert len(bad) == 0, (name, ref, len(bad), bad[:5].tolist())
+        tri, t, counts, _ = r.trace_counts(o, d, reference_bvh=True)
+        assert np.array_equal(tri, g["tri"])
+        assert np.array_equal(counts, g["counts"]), int(np.abs(counts.astype(np.int64) - g["counts"]).sum())
+        # the render path's walk reports the tests it performed (on the large scene far fewer)
+        _, _, fast_counts, _ = r.trace_counts(o, d)
+        assert fast_counts.sum() > 0
+        if name == "standin":
+            assert fast_counts.sum() < counts.sum()
+
+
+def test_lds_ring_spill_path_runs_and_is_exact(tmp_path):
+    """The BVH4 walk's stack beyond the 16-entry LDS ring (HBM spill column; the reference's
+    fixed stack[64] + depth guard, kernel.cu:114, :627-631): on the splinters scene every ray
+    enters nearly every box, the walk spills (counted), and results stay bit-exact vs the
+    oracle -- for batched trace() and for a rendered image."""
+    import oracle as oracle_mod
+    p = scenes.write_splinters(str(tmp_path))
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    s.build_bvh()
+    a = s.arrays()
+    osc = oracle_mod.OracleScene(a)
+    w = h = 24
+    cam = pt.make_camera(width=w, height=h, **scenes.CORNELL_CAMERA)
+    cr = [pt.camera_ray(cam, pt.morton_pxl_to_i(x, y)) for y in range(h) for x in range(w)]
+    o = np.array([c[0] for c in cr], np.float32)
+    d = np.array([c[1] for c in cr], np.float32)
+    sets = ray_sets(a, 1000, 21)
+    o = np.concatenate([o] + [v[0] for v in sets.values()])
+    d = np.concatenate([d] + [v[1] for v in sets.values()])
+    with pt.Renderer(s, 0) as r:
+        tri, t, _, spills = r.trace_counts(o, d)
+        assert spills > 0
+        etri, et = oracle_mod.trace_batch(osc, o, d)
+        assert np.array_equal(tri, etri) and np.array_equal(t.view(np.uint32), et.view(np.uint32))
+        img, st = r.render(cam, w, h, 4, bounces=3, flags=pt.PT_FLAG_COUNT)
+        assert st["spill_entries"] > 0
+        img2, _ = r.render(cam, w, h, 4, bounces=3)
+    ocam = oracle_mod.camera(scenes.CORNELL_CAMERA["pos"], 1.0, 3.0, 0.0, w, h)
+    ref, _ = oracle_mod.render(osc, ocam, w, h, 4, 3, 0, 1234)
+    assert np.array_equal(img.view(np.uint32), img2.view(np.uint32))
+    assert np.array_equal(img.view(np.uint32), ref.astype(np.float32).view(np.uint32))

@@ -1,5 +1,7 @@
 """The CPU oracle (oracle/pt_oracle.c) pinned against the reference's own code and published data:
 - triIntersect / rayAABBIntersect / cameraRay outputs of the reference sources (refgen), bit-exact;
+- trace() (kernel.cu:107-161, the reference's own function compiled by oracle/Makefile): winners,
+  closestT and per-triangle test counts on four scenes incl. the 262K stand-in, bit-exact;
 - the XORWOW recurrence and 2^67 subsequence jump against rocRAND's precomputed matrices;
 - its own committed render fixtures (regression pin) and a brute-force restatement of trace().
 """
@@ -120,6 +122,24 @@ def test_oracle_render_regression(fname, name, w, h, spp, b, i):
     img, cnt = oracle.render(osc, cam, w, h, spp, b, i, 1234)
     assert img.tobytes() == g["img"].tobytes()
     assert cnt["traces"] == int(g["traces"])
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_blob", "quirks", "standin"])
+def test_oracle_trace_matches_reference_trace(name, request):
+    """or_trace == the reference's own trace() (refgen trace, kernel.cu:107-161 compiled from
+    /root/reference) on the committed ray sets: (triIndex, closestT) bit for bit and the test[]
+    increments (kernel.cu:133) per triangle."""
+    g = golden("kat_trace_%s.npz" % name)
+    s = request.getfixturevalue("standin_scene") if name == "standin" else load_scene(name)
+    osc = oracle.OracleScene(s.arrays())
+    assert len(g["counts"]) == len(osc.tris)
+    counts = np.zeros(len(osc.tris), dtype=np.uint32)
+    tri, t = oracle.trace_batch(osc, g["rays"][:, :3], g["rays"][:, 3:], tri_counts=counts)
+    assert np.array_equal(tri, g["tri"])
+    assert np.array_equal(t.view(np.uint32), g["t"].view(np.uint32))
+    assert np.array_equal(counts, g["counts"])
+    names = [str(x) for x in g["set_names"]]
+    assert {"axis", "tiny", "outside", "vertex_planes", "bounce"} <= set(names)
 
 
 def test_trace_equals_bruteforce_restatement():

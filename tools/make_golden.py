@@ -14,6 +14,12 @@ Outputs (all small, committed):
   kat_tone.npz                       PPM tone map (int)(gammaCorrect(normalized(c), 1/2.2) * 255)
   xorwow.npz                         oracle XORWOW streams (regression pin)
   render_*.npz                       oracle f64 mean images for small configs (regression pin)
+  kat_trace_<scene>.npz              the reference's own trace() (kernel.cu:107-161, compiled from
+                                     /root/reference/kernel.cu by oracle/Makefile) on the ray sets of
+                                     tests/raysets.py: (triIndex, t) per ray + per-triangle test[]
+                                     counts (kernel.cu:133) summed over the rays
+
+`python tools/make_golden.py --only trace` regenerates only the kat_trace_* files.
 """
 from __future__ import annotations
 
@@ -34,6 +40,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 from cudapathtracer_amd import scenes  # noqa: E402
 from cudapathtracer_amd.api import MAT, NODE, TRI, VEC3  # noqa: E402
 import oracle  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from raysets import bounce_rays, ray_sets  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 SCENES = os.path.join(GOLD, "scenes")
@@ -200,9 +208,62 @@ def render_fixtures():
                             img=img, traces=np.uint64(cnt["traces"]))
 
 
+def ref_trace(tmp, rays, loads, cwd):
+    """(tri, t, counts) from the reference's trace() on the scene of `loads` (refgen trace)."""
+    rin, rout, rcnt = (os.path.join(tmp, "trace." + k) for k in ("in", "out", "cnt"))
+    np.ascontiguousarray(rays, dtype=np.float32).tofile(rin)
+    args = ["trace", rin, rout, rcnt]
+    for obj, origin, scale, flip in loads:
+        args += [obj, origin[0], origin[1], origin[2], scale, flip]
+    run_ref(args, cwd=cwd)
+    res = np.fromfile(rout, "<i4").reshape(-1, 2)
+    return res[:, 0].copy(), res[:, 1].copy().view(np.float32), np.fromfile(rcnt, "<u4")
+
+
+def kat_trace(tmp):
+    """trace() goldens: the ray sets of tests/raysets.py plus first-bounce rays off the interior
+    set's hits; for the stand-in, camera rays of the bench view and their bounces first."""
+    jobs = [(name, SCENE_SETS[name], SCENES, 1024, None) for name in ("cornell", "cornell_blob", "quirks")]
+    gen = os.path.join(tmp, "gen_trace")
+    p = scenes.write_sponza_standin(gen)
+    jobs.append(("standin", [(os.path.relpath(p, gen), (0, 0, 0), 1.0, 0)], gen, 512, p))
+    for name, loads, cwd, n, standin in jobs:
+        arrs = ref_scene(tmp, name, loads) if standin is None else None
+        if standin is not None:
+            import cudapathtracer_amd as pt
+            s = pt.Scene()
+            s.load_obj(standin, mtl_basepath=os.path.dirname(standin) + "/")
+            s.build_bvh()
+            arrs = s.arrays()
+        sets = []
+        if standin is not None:
+            import cudapathtracer_amd as pt
+            c = scenes.SPONZA_STANDIN_CAMERA
+            cam = pt.make_camera(c["pos"], c["dist_from_film"], c["focal_length"], 0.0, 1920, 1080)
+            idx = np.random.default_rng(9).integers(0, 1920 * 1080, 4 * n)
+            cr = [pt.camera_ray(cam, int(i), lens=False) for i in idx]
+            sets.append(("camera", np.array([r[0] for r in cr], np.float32), np.array([r[1] for r in cr], np.float32)))
+        for k, (o, d) in ray_sets(arrs, n, 5 if standin is None else 11).items():
+            sets.append((k, o, d))
+        first = sets[0]
+        tri0, t0, _ = ref_trace(tmp, np.concatenate([first[1], first[2]], 1), loads, cwd)
+        bo, bd = bounce_rays(arrs, first[1], first[2], tri0, t0, 6 if standin is None else 10)
+        sets.append(("bounce", bo, bd))
+        rays = np.concatenate([np.concatenate([o, d], 1) for _, o, d in sets]).astype(np.float32)
+        tri, t, counts = ref_trace(tmp, rays, loads, cwd)
+        offs = np.cumsum([0] + [len(o) for _, o, _ in sets]).astype(np.int64)
+        np.savez_compressed(os.path.join(GOLD, "kat_trace_%s.npz" % name), rays=rays, tri=tri, t=t, counts=counts,
+                            set_names=np.array([k for k, _, _ in sets]), set_offsets=offs)
+        print("kat_trace", name, len(rays), "rays,", int((tri >= 0).sum()), "hits,", int(counts.sum()), "tests")
+
+
 def main():
     if not os.path.exists(REFGEN):
         sys.exit("oracle/_ref/refgen missing: run `make -C oracle` with /root/reference present")
+    if sys.argv[1:] == ["--only", "trace"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            kat_trace(tmp)
+        return
     os.makedirs(GOLD, exist_ok=True)
     if os.path.isdir(SCENES):
         shutil.rmtree(SCENES)
@@ -235,6 +296,7 @@ def main():
         kat_cam(tmp, rng)
         kat_morton(tmp)
         kat_tone(tmp, rng)
+        kat_trace(tmp)
     xorwow_fixture()
     render_fixtures()
     print("golden fixtures written to", GOLD)
