@@ -10,7 +10,9 @@ of the per-GPU work is NOT used: total work per step is fixed, so scaling is "st
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with:
   value      = Msamples/s, whole job (pixel samples per second)
-  roofline   = algorithmic bytes of the render kernel / its measured duration vs 8 TB/s HBM
+  roofline   = measured memory-side bytes per launch (rocprof, calibrated; from profiles/traffic.json
+               when it matches this kernel) / this run's kernel time vs 8 TB/s HBM, with the
+               algorithmic bytes and the binding pipes beside it
   cpu_baseline = the CPU oracle (same integrator) on a bounded pixel subset, host cores
 """
 from __future__ import annotations
@@ -29,7 +31,42 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 NODE_BYTES = 128          # one BVH4 node record (6 x float4 child boxes + uint4 children + pad)
-ACCEL_TAG = "bvh4-leafmask-tailsplit-v4"   # profiles/traffic.json is used only when it was measured on this kernel
+TRI_BYTES = 48            # one triangle record {v0, e1, e2, id, rank, parent}
+# the sources that define the render kernel: profiles/traffic.json is used only when it was measured
+# on a build of exactly these (a stale PMC number cannot ride along)
+KERNEL_SOURCES = ("cudapathtracer_amd/csrc/hip/pt_render.hip", "cudapathtracer_amd/csrc/hip/pt_device.h",
+                  "cudapathtracer_amd/csrc/Makefile")
+
+
+def kernel_source_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def host_cores():
+    """Threads for the CPU baseline, as `nproc` counts them: OMP_NUM_THREADS when set, else the
+    CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.strip().isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def log(*a):
@@ -82,10 +119,55 @@ def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
     samples = len(pix) * spp
     return {
         "value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+        "nproc": host_cores(), "cpu_model": cpu_model(),
         "mrays_per_s": cnt["traces"] / dt / 1e6,
         "sample": "%d pixels (every %d-th 8x8 tile) x %d spp of the same %dx%d image, %.1fs"
                   % (len(pix), stride, spp, width, height, dt),
     }
+
+
+def roofline(counts, kms, W, H, args, world):
+    """The render kernel against the HBM roofline.
+
+    achieved / frac / traffic: MEASURED memory-side bytes per launch (rocprofv3 FETCH_SIZE x2 +
+    WRITE_SIZE, the x2 calibrated on this kernel's own access shapes, profiles/r02_fetch_calibration)
+    from profiles/traffic.json -- used only if that profile was taken on this exact kernel source and
+    config -- over this run's kernel time; null otherwise.  The algorithmic bytes (node records
+    fetched from memory, i.e. not from the LDS copy of the top nodes, + triangle records + per-ray
+    shading reads + output) are reported beside it: caches serve much of them, so their rate is not
+    an HBM figure.  binding: the pipes that actually limit the kernel, from the same profile."""
+    npx = counts["samples"] / max(args.spp, 1)
+    mem_nodes = counts["node_tests"] - counts["lds_node_tests"]
+    alg = (mem_nodes * NODE_BYTES + counts["tri_tests"] * TRI_BYTES + counts["rays_traced"] * (16 + 48) + npx * 12)
+    sec = kms * 1e-3
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+            "traffic_source": None,
+            "algorithmic_bytes_per_launch": int(alg), "algorithmic_gbs": round(alg / sec / 1e9, 2),
+            "kernel": "render_unidir_wf" if args.integrator == 0 and not (args.flags & 1) else "render_tiles",
+            "kernel_ms": round(kms, 3), "kernel_source_sha256": kernel_source_sha256(),
+            "node_fetches": int(counts["node_tests"]), "lds_node_fetches": int(counts["lds_node_tests"]),
+            "tri_tests": int(counts["tri_tests"]),
+            "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
+            "leaf_step_frac": round(counts["leaf_steps"] / max(counts["node_tests"], 1), 4),
+            "accel_fallbacks": int(counts["accel_fallbacks"]), "spill_entries": int(counts["spill_entries"]),
+            "walk_phase_frac": round(counts["walk_cycles"] / max(counts["walk_cycles"] + counts["shade_cycles"], 1), 4),
+            "shade_phases": int(counts["shade_lane_slots"] // 64)}
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+        except (OSError, ValueError):
+            tj = {}
+        if (tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, max(world, args.sim_shards)]
+                and tj.get("kernel_source_sha256") == roof["kernel_source_sha256"]):
+            traffic = int(tj["traffic_bytes_per_launch"])
+            roof["traffic"] = traffic
+            roof["achieved"] = round(traffic / sec / 1e9, 2)
+            roof["frac"] = round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4)
+            roof["traffic_source"] = {"profile": tj.get("profile"), "method": tj.get("method"),
+                                      "kernel_ms_profiled": tj.get("kernel_ms")}
+            if tj.get("binding"):
+                roof["binding"] = tj["binding"]
+    return roof
 
 
 def main():
@@ -101,7 +183,7 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=host_cores())
     ap.add_argument("--no-count", action="store_true", help="skip the counting pass (roofline bytes)")
     ap.add_argument("--sim-shards", type=int, default=1,
                     help="diagnostic, single process only: render shard 0 of N (one GPU's share at N GPUs)")
@@ -180,38 +262,7 @@ def main():
         finite = bool(np.isfinite(img).all())
         ms_step = elapsed / args.steps * 1e3
         kms = float(np.mean(kernel_ms))
-        roof = None
-        if counts is not None:
-            # algorithmic bytes per launch: 128-B BVH4 node records visited + 48-B triangle records
-            # tested + per traced ray 16 B hit-shading record + 48 B material + 12 B/pixel output
-            npx = counts["samples"] / max(args.spp, 1)
-            bytes_launch = (counts["node_tests"] * NODE_BYTES + counts["tri_tests"] * 48 +
-                            counts["rays_traced"] * (16 + 48) + npx * 12)
-            achieved = bytes_launch / (kms * 1e-3) / 1e9
-            traffic = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    tj = json.load(open(args.traffic_json))
-                    if (tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, world]
-                            and tj.get("accel") == ACCEL_TAG):
-                        traffic = tj.get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    # node/triangle bytes are mostly served by L2/MALL, so the
-                    # algorithmic rate can exceed what HBM alone delivers (frac > 1); the HBM
-                    # share is the measured traffic over the kernel time
-                    "hbm_frac": (round(traffic / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None),
-                    "note": "algorithmic bytes include L2/MALL hits; the kernel is co-bound by VALU issue and the per-lane vector-memory address pipeline (TA/TCP), not by HBM (DESIGN.md 6)",
-                    "algorithmic_bytes_per_launch": int(bytes_launch), "kernel": "render_unidir_wf" if args.integrator == 0 and not (args.flags & 1) else "render_tiles",
-                    "kernel_ms": round(kms, 3),
-                    "node_fetches": int(counts["node_tests"]), "tri_tests": int(counts["tri_tests"]),
-                    "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
-                    "leaf_step_frac": round(counts["leaf_steps"] / max(counts["node_tests"], 1), 4),
-                    "accel_fallbacks": int(counts["accel_fallbacks"]),
-                    "walk_phase_frac": round(counts["walk_cycles"] / max(counts["walk_cycles"] + counts["shade_cycles"], 1), 4),
-                    "shade_phases": int(counts["shade_lane_slots"] // 64)}
+        roof = roofline(counts, kms, W, H, args, world) if counts is not None else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget)

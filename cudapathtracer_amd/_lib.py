@@ -21,6 +21,7 @@ PT_FLAG_NO_DEAD_PATH_SKIP = 0x2
 PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
+PT_FLAG_TRI_COUNTS = 0x20
 PT_LIGHT_SPHERE = 0x80000000     # lights[] entry of an emissive sphere
 ABI_VERSION = 5                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
@@ -70,7 +71,8 @@ class Stats(C.Structure):
                 ("rays_traced", C.c_uint64), ("rays_reference", C.c_uint64), ("rays_nominal", C.c_uint64),
                 ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("walk_lane_slots", C.c_uint64),
                 ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64),
-                ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64), ("spill_entries", C.c_uint64)]
+                ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64), ("spill_entries", C.c_uint64),
+                ("lds_node_tests", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -123,7 +123,7 @@ int main(int argc, char** argv)
     if (objs.empty()) usage("at least one --obj is required");
     if (gpus < 1) usage("--gpus must be >= 1");
     if (!tri_csv.empty() && gpus != 1) usage("--tri-counts needs --gpus 1");
-    if (!tri_csv.empty()) p.flags |= PT_FLAG_COUNT;
+    if (!tri_csv.empty()) p.flags |= PT_FLAG_COUNT | PT_FLAG_TRI_COUNTS;
     // --reference-walk: the reference's own trace() sequence for every sample (its node order, the
     // camera ray traced per sample, dead paths traced), so --tri-counts reproduces its out.csv
     if (ref_walk) p.flags |= PT_FLAG_REFERENCE_TRAVERSAL | PT_FLAG_NO_PRIMARY_CACHE | PT_FLAG_NO_DEAD_PATH_SKIP;

@@ -575,20 +575,23 @@ __device__ __forceinline__ bool walk4_begin(W4& w, V3 o, V3 d, const float* root
 // Conservative test of two child boxes (packed: one v_pk_fma_f32 per plane pair).  The near /
 // far planes were picked per ray by the load offsets, so t_near <= t_far per axis already (FMA
 // rounding is monotonic and lo <= hi): the entry is max3 of the near values, the exit min3 of the
-// far ones, and no NaN can arise (finite bounds, |inv| <= 2^100).  Returns max(entry, -cull_abs)
-// (+inf = not entered): the box is entered iff max(entry, -cull_abs) <= min(exit, limit), which is
-// entry <= exit && exit >= -cull_abs && entry <= limit.  Entries below -cull_abs only sort first.
+// far ones, and no NaN can arise (finite bounds, |inv| <= 2^100).  A box is entered iff
+// max(entry, 0) <= min(exit, limit), i.e. entry <= exit, exit >= 0 and entry <= limit.
+// Clamping at 0 (not at -cull_abs) is conservative: a triangle the reference accepts (t > 0) lies
+// inside its box, which is inflated by the margin m (accel_build.cpp), so the exit is >= t + m > 0
+// exactly and the computed exit's rounding error (~2^-23 of the plane magnitudes) is far below m.
+// The clamped entry (>= 0) is also the stack key's distance.
 __device__ __forceinline__ f2 pk_fma(f2 a, float b, float c)
 {
     return __builtin_elementwise_fma(a, f2{b, b}, f2{c, c});
 }
 // max/min of values known not to be NaN, as bare v_max3/v_min3 (IEEE mode would otherwise
 // canonicalize each operand the compiler cannot prove canonical, e.g. packed-FMA halves).
-__device__ __forceinline__ float entry4(float a, float b, float c, float cull_abs)
+__device__ __forceinline__ float entry4(float a, float b, float c)
 {
     float m, r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
-    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(r) : "s"(cull_abs), "v"(m));
+    asm("v_max_f32_e32 %0, 0, %1" : "=v"(r) : "v"(m));
     return r;
 }
 __device__ __forceinline__ float exit4(float a, float b, float c, float limit)
@@ -598,15 +601,16 @@ __device__ __forceinline__ float exit4(float a, float b, float c, float limit)
     asm("v_min_f32_e32 %0, %1, %2" : "=v"(r) : "v"(limit), "v"(m));
     return r;
 }
+// entry distances (>= 0) and entered flags of two children
 __device__ __forceinline__ void box_enter2(const W4& w, f2 nx, f2 ny, f2 nz, f2 fx, f2 fy, f2 fz, float limit,
-                                           float cull_abs, float& t0, float& t1)
+                                           float& t0, float& t1, bool& e0, bool& e1)
 {
     const f2 ax = pk_fma(nx, w.inv.x, -w.oi.x), ay = pk_fma(ny, w.inv.y, -w.oi.y), az = pk_fma(nz, w.inv.z, -w.oi.z);
     const f2 bx = pk_fma(fx, w.inv.x, -w.oi.x), by = pk_fma(fy, w.inv.y, -w.oi.y), bz = pk_fma(fz, w.inv.z, -w.oi.z);
-    const float n0 = entry4(ax.x, ay.x, az.x, cull_abs), n1 = entry4(ax.y, ay.y, az.y, cull_abs);
-    const float f0 = exit4(bx.x, by.x, bz.x, limit), f1 = exit4(bx.y, by.y, bz.y, limit);
-    t0 = (n0 <= f0) ? n0 : INFINITY;
-    t1 = (n1 <= f1) ? n1 : INFINITY;
+    t0 = entry4(ax.x, ay.x, az.x);
+    t1 = entry4(ax.y, ay.y, az.y);
+    e0 = t0 <= exit4(bx.x, by.x, bz.x, limit);
+    e1 = t1 <= exit4(bx.y, by.y, bz.y, limit);
 }
 // x * 48 as (x << 5) + (x << 4): two full-rate ops instead of a quarter-rate v_mul_lo_u32
 __device__ __forceinline__ uint32_t mul48(uint32_t x)
@@ -765,15 +769,15 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         const float lim = w.best_t * cull_rel;
         // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
         float t0, t1, t2, t3;
+        bool e0, e1, e2, e3;
         box_enter2(w, f2{NX.x, NX.y}, f2{NY.x, NY.y}, f2{NZ.x, NZ.y}, f2{FX.x, FX.y}, f2{FY.x, FY.y}, f2{FZ.x, FZ.y},
-                   lim, cull_abs, t0, t1);
+                   lim, t0, t1, e0, e1);
         box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
-                   lim, cull_abs, t2, t3);
+                   lim, t2, t3, e2, e3);
         uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
         // entered leaf children as one queue entry: their slots are consecutive from child 0's
         // (leaf children come first), so the entry is child 0's slot and a 4-bit mask
         // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
-        const bool e0 = t0 != INFINITY, e1 = t1 != INFINITY, e2 = t2 != INFINITY, e3 = t3 != INFINITY;
         const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
         const uint32_t lm = (e0 && l0 ? 1u : 0u) | (e1 && l1 ? 2u : 0u) | (e2 && l2 ? 4u : 0u) | (e3 && l3 ? 8u : 0u);
         if (lm != 0u) {
@@ -781,12 +785,12 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             if (!leaf4_pending(w)) w.leaf = e;
             else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
         }
-        // inner children, nearest first.  Each entered inner child becomes its stack entry
-        // (max(entry, 0) truncated to the bits above node_mask | node index): non-negative floats
+        // inner children, nearest first.  Each entered inner child becomes its stack entry (entry
+        // distance, >= 0, truncated to the bits above node_mask | node index): non-negative floats
         // order like their bit patterns, so four u32 min/max pairs sort the entries by distance;
         // leaves and boxes not entered become ~0 and sort last.
         auto key = [&](float t, uint32_t r, bool e, bool l) -> uint32_t {
-            return (e && !l) ? (((uint32_t)max((int32_t)__float_as_uint(t), 0) & ~node_mask) | r) : kNone;
+            return (e && !l) ? ((__float_as_uint(t) & ~node_mask) | r) : kNone;
         };
         uint32_t k0 = key(t0, r0, e0, l0), k1 = key(t1, r1, e1, l1), k2 = key(t2, r2, e2, l2), k3 = key(t3, r3, e3, l3);
         auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };

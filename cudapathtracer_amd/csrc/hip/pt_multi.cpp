@@ -100,6 +100,7 @@ void add_stats(pt_stats* sum, const pt_stats& s)
     sum->walk_cycles += s.walk_cycles;
     sum->shade_cycles += s.shade_cycles;
     sum->spill_entries += s.spill_entries;
+    sum->lds_node_tests += s.lds_node_tests;
 }
 
 }  // namespace

@@ -1895,7 +1895,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
     HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
-    if (count) {   // per-triangle test counts of this render (read back with pt_tri_counts)
+    if (count && (p->flags & PT_FLAG_TRI_COUNTS)) {   // per-triangle test counts of this render (pt_tri_counts)
         HIP_TRY(hipMemsetAsync(c->tri_counts, 0, (size_t)std::max<uint32_t>(c->num_tris, 1u) * 4, stream));
         a.tri_counts = c->tri_counts;
     }
@@ -2078,6 +2078,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         st->walk_cycles = cnt[9];
         st->shade_cycles = cnt[10];
         st->spill_entries = cnt[25];
+        st->lds_node_tests = cnt[13];
         const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
         st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
     }

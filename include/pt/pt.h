@@ -144,9 +144,11 @@ typedef struct pt_ctx pt_ctx;
                                              the exact node/triangle sequence of kernel.cu:112-161 */
 #define PT_FLAG_NO_DEAD_PATH_SKIP 0x2u    /* trace every bounce even after the path weight is 0   */
 #define PT_FLAG_NO_PRIMARY_CACHE 0x4u     /* re-trace the (sample-invariant) camera ray per sample  */
-#define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant), incl.
-                                             the per-triangle counts of kernel.cu:133 (pt_tri_counts) */
+#define PT_FLAG_COUNT 0x8u                /* fill node/triangle test counters (slower variant)     */
 #define PT_FLAG_REFERENCE_BVH 0x10u       /* culled walk on the reference BVH only (no SAH BVH)     */
+#define PT_FLAG_TRI_COUNTS 0x20u          /* with PT_FLAG_COUNT: also the per-triangle test counts of
+                                             kernel.cu:133 (read back with pt_tri_counts; one atomic
+                                             per triangle test)                                      */
 
 typedef struct {
     int32_t width, height;   /* image size (IMAGE_WIDTH/HEIGHT, kernel.cu:28-29)                    */
@@ -185,6 +187,8 @@ typedef struct {
     uint64_t spill_entries;    /* PT_FLAG_COUNT, BVH4 walk: stack entries pushed beyond the 16-entry
                                   per-lane LDS ring into the lane's HBM spill column (the reference's
                                   fixed stack[64] of kernel.cu:114 has no such tier)              */
+    uint64_t lds_node_tests;   /* PT_FLAG_COUNT, wavefront kernel: the node_tests served by the copy
+                                  of the BVH4's top nodes in LDS (no vector-memory fetch)         */
 } pt_stats;
 
 /* Host-only diagnostic: builds the render path's private acceleration structure for `scene`
@@ -221,7 +225,7 @@ int pt_trace_counts(pt_ctx* ctx, uint32_t n, const float* rays, int32_t* tri_out
                     uint32_t* tri_counts, uint64_t* spill_entries);
 
 /* Per-triangle test counts (n = num_tris entries, by original triangle id) of the ctx's last
- * pt_render / pt_render_device with PT_FLAG_COUNT: the reference's bvhIntersection buffer
+ * pt_render / pt_render_device with PT_FLAG_COUNT | PT_FLAG_TRI_COUNTS: the reference's bvhIntersection buffer
  * (kernel.cu:694-697, written to out.csv at :742-750).  With PT_FLAG_REFERENCE_TRAVERSAL |
  * PT_FLAG_NO_PRIMARY_CACHE | PT_FLAG_NO_DEAD_PATH_SKIP the render performs exactly the reference's
  * trace() calls, so these are the reference's counts (without its racy increments and with the

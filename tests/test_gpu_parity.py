@@ -262,7 +262,7 @@ def test_per_triangle_counts_match_reference(oracle_mod, cb, integ):
     w, h, spp = 24, 16, 3
     cam = pt.make_camera(width=w, height=h, **CAM)
     flags = (pt.PT_FLAG_REFERENCE_TRAVERSAL | pt.PT_FLAG_NO_PRIMARY_CACHE | pt.PT_FLAG_NO_DEAD_PATH_SKIP |
-             pt.PT_FLAG_COUNT)
+             pt.PT_FLAG_COUNT | pt.PT_FLAG_TRI_COUNTS)
     img, st = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=flags)
     counts = r.tri_counts()
     osc = oracle_mod.OracleScene(s.arrays())
@@ -273,7 +273,7 @@ def test_per_triangle_counts_match_reference(oracle_mod, cb, integ):
     assert np.array_equal(counts, ocounts)
     assert int(counts.sum()) == st["tri_tests"] == cnt["tri_tests"]
     # the fast path's own counts: fewer tests, same image
-    img2, st2 = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=pt.PT_FLAG_COUNT)
+    img2, st2 = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=pt.PT_FLAG_COUNT | pt.PT_FLAG_TRI_COUNTS)
     fast = r.tri_counts()
     assert _bits_equal(img2, ref) == 0
     assert 0 < int(fast.sum()) < int(counts.sum())

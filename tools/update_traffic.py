@@ -1,23 +1,54 @@
 #!/usr/bin/env python3
-"""profiles/traffic.json from a profile's pmc_summary.json: HBM-side bytes per launch of the render
-kernel (FETCH_SIZE x2 per the gfx950 correction of MI355X_MICROARCH.md + WRITE_SIZE), which bench.py
-reports as roofline.traffic when its config and accel tag match."""
+"""profiles/traffic.json from a profile's pmc_summary.json (tools/summarize_profile.py output).
+
+traffic = FETCH_SIZE x 2 + WRITE_SIZE per launch of the render kernel, in bytes: rocprofv3 reports
+both in KB; the x2 is the gfx950 correction of MI355X_MICROARCH.md, calibrated on this kernel's own
+access shapes (node / triangle gathers, lane-major record cells: profiles/r02_fetch_calibration).
+The file is stamped with the render kernel's source hash (bench.kernel_source_sha256) and the bench
+config, so bench.py uses it only for the kernel and workload it was measured on.
+
+usage: tools/update_traffic.py profiles/<tag> [W H SPP BOUNCES INTEGRATOR SHARDS]
+"""
 import json
+import os
 import sys
 
-src, accel = sys.argv[1], sys.argv[2]
-p = json.load(open(src))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+prof = sys.argv[1]
+cfg = [int(x) for x in sys.argv[2:8]] if len(sys.argv) >= 8 else [1920, 1080, 256, 3, 0, 1]
+p = json.load(open(os.path.join(prof, "pmc_summary.json")))
 c = p["counters_per_launch"]
+durs = sorted(p["kernel_trace_durations_ns"])
+kms = durs[len(durs) // 2] / 1e6 if durs else None
 out = {
-    "config": [1920, 1080, 256, 3, 0, 1],
-    "accel": accel,
+    "config": cfg,
     "kernel": p["kernels"][0] if p["kernels"] else "render_unidir_wf",
+    "kernel_source_sha256": bench.kernel_source_sha256(),
+    "profile": os.path.relpath(prof, ROOT),
+    "kernel_ms": kms,
     "fetch_size_kb": c["FETCH_SIZE"],
     "write_size_kb": c["WRITE_SIZE"],
-    "hbm_bytes_per_launch": int(c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024),
-    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (one launch each); FETCH_SIZE "
-              "x1024 (KB->B) x2 (gfx950 reports 1/2 of wide reads, MI355X_MICROARCH.md HBM) + WRITE_SIZE x1024",
-    "source": src,
+    "traffic_bytes_per_launch": int(c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024),
+    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (one launch each): "
+              "FETCH_SIZE x1024 x2 + WRITE_SIZE x1024 (x2 calibrated on the kernel's gather shapes, "
+              "profiles/r02_fetch_calibration)",
 }
-json.dump(out, open("profiles/traffic.json", "w"), indent=1)
+if "GRBM_GUI_ACTIVE" in c:
+    cyc = c["GRBM_GUI_ACTIVE"] / 8.0     # summed over the 8 XCDs
+    b = {"limiter": "valu+vmem-issue", "cycles_per_launch": int(cyc)}
+    if "SQ_INSTS_VALU" in c:
+        b["valu_frac"] = round(c["SQ_INSTS_VALU"] * 4 / (1024 * cyc), 4)   # wave64 VALU op = 4 SIMD cycles
+    if "TD_TD_BUSY_sum" in c:
+        b["td_busy"] = round(c["TD_TD_BUSY_sum"] / 256 / cyc, 4)
+    if "TA_TA_BUSY_sum" in c:
+        b["ta_busy"] = round(c["TA_TA_BUSY_sum"] / 256 / cyc, 4)
+    if "TD_TC_STALL_sum" in c:
+        b["td_tc_stall"] = round(c["TD_TC_STALL_sum"] / 256 / cyc, 4)
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        b["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
+    out["binding"] = b
+json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
