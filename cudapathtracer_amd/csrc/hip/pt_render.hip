@@ -80,6 +80,8 @@ struct Args {
     uint32_t num_tris;
     uint32_t sphere_mat_base;       // material of sphere i = mats[sphere_mat_base + i]
     uint32_t* tri_counts;           // PT_FLAG_COUNT: per-triangle test counts by original id (kernel.cu:133)
+    const DTri* emis;               // last-bounce light probe: the emissive triangles' records (see begin_trace)
+    uint32_t num_emis;              // 0 = probe off
 };
 
 __device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
@@ -615,6 +617,10 @@ __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hi
 // Per-unit words of init_pixel_states' output beyond the XORWOW state (words 0..5: v0..v4, d)
 enum : uint32_t { UW_PXY = 6, UW_N0, UW_NEND, UW_TQ, UW_CD, kUnitWords = UW_CD + 3 };
 constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the image
+constexpr uint32_t kMaxProbeEmitters = 4;    // last-bounce light probe: at most this many emissive triangles
+// LDS of a wavefront block after the counters: the probe's emitter count (16 B) and records, then the
+// staged BVH4 top nodes
+constexpr uint32_t kProbeLdsBytes = 16 + kMaxProbeEmitters * (uint32_t)sizeof(DTri);
 __device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c, uint32_t chunks)
 {
     return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / chunks);
@@ -737,7 +743,7 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 // Counting variant only: SEC(k) counts the waves that execute section k of the shading code
 // (counters[32 + k]; a profile of where shading issue slots go -- DESIGN.md "Measurement").
 enum : int { SEC_PASS = 0, SEC_CHECK, SEC_SLOW, SEC_BOUNCE, SEC_EMIT, SEC_COSINE, SEC_LIGHT, SEC_SAMPLE_END,
-             SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, kSections = 16 };
+             SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, SEC_PROBE, kSections = 16 };
 constexpr int kHist = 16;   // counting variant: walk steps per ray, log2 buckets (counters[48 + b])
 #ifdef PT_SEC_MARKERS   // analysis builds: mark the sections in the ISA listing
 #define SEC_MARK(k) asm volatile("; SEC " #k)
@@ -754,11 +760,25 @@ constexpr int kHist = 16;   // counting variant: walk steps per ray, log2 bucket
         }                                                                                        \
     } while (0)
 
-template <bool kCount>
-__device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
-                                           int32_t& htri, float& ht, W4& w, const Stack4& S,
-                                           unsigned long long* lcnt)
+// The kernel arguments as the shading pass reads them: from the kernarg segment (render_unidir_wf's
+// only explicit argument, at offset 0) through a pointer made opaque at the pass's start, so that the
+// scalar loads of the shading-only fields cannot be hoisted to the kernel's entry -- which would keep
+// dozens of SGPRs live across the walk loop and push the walk's own values into SGPR spills.
+typedef const __attribute__((address_space(4))) Args KArgs;
+__device__ __forceinline__ const Args& kernel_args_opaque()
 {
+    KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const Args*)p;
+}
+
+template <bool kCount>
+__device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
+                                           int32_t& htri, float& ht, W4& w, const Stack4& S,
+                                           unsigned long long* lcnt, const uint32_t* lprobe)
+{
+    (void)a_in;
+    const Args& a = kernel_args_opaque();
     const int D = a.bounces;
     SEC(SEC_PASS);
     if (state == ST_CHECK) {
@@ -779,15 +799,19 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
     C3 wgt = c3(dbl(k2.x, k2.y), dbl(k2.z, k2.w), dbl(k3.x, k3.y));
 
     // begin a trace of (o, d); true = the lane continues shading at once (root miss, or
-    // a ray outside the Markstein preconditions, which takes the exact slow walk)
-    auto begin_trace = [&](V3 o, V3 d) -> bool {
+    // a ray outside the Markstein preconditions, which takes the exact slow walk).  bound: the walk
+    // accepts hits with t < bound (kMaxFloat: a plain trace; see the light probe below)
+    auto begin_trace = [&](V3 o, V3 d, float bound) -> bool {
         wave_count(lcnt + 0, lane);
         SEC(SEC_BEGIN);
         if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }   // spheres only
         if (!((a.scene_fast != 0u) && ray_fast(o, d))) { state = ST_SLOW; return true; }
         if (!walk4_begin(w, o, d, a.acc_root, a.cull_abs)) {
-            htri = -1; ht = kMaxFloat; state = ST_SHADE; return true;
+            htri = -1; ht = kMaxFloat;
+            state = (bound == kMaxFloat) ? ST_SHADE : ST_SLOW;
+            return true;
         }
+        w.best_t = bound;
         state = ST_TRACE;
         return false;
     };
@@ -836,7 +860,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
             }
         }
         fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
-        return begin_trace(ro, rd);
+        return begin_trace(ro, rd, kMaxFloat);
     };
 
     // A lane whose samples need no trace (primary memo hit on an emitter or a miss: the path is
@@ -1020,6 +1044,31 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 again = start_sample(px, py);
                 break;
             }
+            // Last-bounce light probe.  The hit of bounce D-1 only decides the emission it adds
+            // (weight * Le if its material has emission.r != 0, kernel.cu:453); its position, normal
+            // and next direction are never used, and the draws that follow do not depend on it (u,
+            // then 2 or 3).  a.emis holds every triangle whose material has emission.r != 0 (the
+            // integrator's own test, not the caller's light list); each is tested exactly (the
+            // walk's triIntersect bits):
+            //  * no hit with 0 < t < MAX_FLOAT: the reference's winner is not emissive (or there is
+            //    none), so the bounce adds 0 -- the path is dead: replay its draws, no trace at all;
+            //  * otherwise the winner has t <= t_min (the emitter at t_min is a triangle the reference
+            //    may test; if it does not, the final winner check sends the ray to the exact slow
+            //    walk), so the walk starts with its bound at t_min instead of MAX_FLOAT.
+            float bound = kMaxFloat;
+            const uint32_t nem = lprobe[0];   // (the emitters are staged in the block's LDS)
+            if (i == D - 1 && nem != 0u && !(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && !czero(wgt) &&
+                a.scene_fast != 0u && ray_fast(ro, rd)) {
+                SEC(SEC_PROBE);
+                float bt = kMaxFloat;
+                const float4* er = reinterpret_cast<const float4*>(lprobe + 4);
+                for (uint32_t k = 0; k < nem; ++k, er += 3) {
+                    const float t = tri_hit_pk(f2{ro.x, ro.y}, ro.z, f2{rd.x, rd.y}, rd.z, er[0], er[1], er[2].x);
+                    if (0.0f < t && t < bt) bt = t;
+                }
+                if (bt == kMaxFloat) wgt = c3(0.0, 0.0, 0.0);   // adds nothing: dead from here
+                else bound = __uint_as_float(__float_as_uint(bt) + 1u);   // the next float above t_min
+            }
             if (!(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP) && czero(wgt)) {   // dead path: replay the draws
                 wave_count(lcnt + 1, lane);
                 SEC(SEC_DEAD);
@@ -1030,7 +1079,7 @@ __device__ __forceinline__ void shade_lane(const Args& a, const ColdRec& R, int 
                 continue;
             }
             wave_count(lcnt + 1, lane);
-            again = begin_trace(ro, rd);
+            again = begin_trace(ro, rd, bound);
             break;
         }
     }
@@ -1127,8 +1176,12 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.lane_off = &R.voff;
     S.off_mask = ~0u;
     S.off_shift = 2;
-    // the top of the BVH4 in LDS (after the rings and counters; kTopNodeBytes per node)
-    float4* const ltop = reinterpret_cast<float4*>(lcnt + 4 + (kSections + kHist) / 2);
+    // the light probe's emitters (count, then records), then the top of the BVH4 (kTopNodeBytes per node)
+    uint32_t* const lprobe = reinterpret_cast<uint32_t*>(lcnt + 4 + (kSections + kHist) / 2);
+    if (threadIdx.x == 0) lprobe[0] = a.num_emis;
+    for (uint32_t k = threadIdx.x; k < a.num_emis * 3; k += blockDim.x)
+        reinterpret_cast<float4*>(lprobe + 4)[k] = reinterpret_cast<const float4*>(a.emis)[k];
+    float4* const ltop = reinterpret_cast<float4*>(reinterpret_cast<char*>(lprobe) + kProbeLdsBytes);
     for (uint32_t k = threadIdx.x; k < a.top_nodes * (kTopNodeBytes / 16); k += blockDim.x) {
         const uint32_t nd = k / (kTopNodeBytes / 16), q = k - nd * (kTopNodeBytes / 16);
         ltop[k] = reinterpret_cast<const float4*>(a.nodes4 + nd)[q];
@@ -1170,7 +1223,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 if (!more) {
                     // the winner's check against the reference BVH runs in the shading phase
                     // (htri, ht) == (w.best_slot, w.best_t): the hit is already in place
-                    state = (w.best_slot == kNone) ? ST_SHADE : ST_CHECK;
+                    // (no winner: a miss -- or, for a bounded last-bounce walk, never expected: exact slow walk)
+                    state = (w.best_slot != kNone) ? ST_CHECK : (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
                 }
             }
         }
@@ -1187,7 +1241,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (kCount) ++shade_slots;
         // (the lane id is recomputed for the shading pass: one VGPR less live across the walk loop)
         if (state != ST_TRACE && state != ST_DONE)
-            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt);
+            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
@@ -1446,6 +1500,8 @@ struct pt_ctx {
     int32_t acc4_depth = 0;
     uint32_t node4_mask = 0;
     uint32_t* tri_counts = nullptr;   // PT_FLAG_COUNT: per-triangle test counts (num_tris entries, >= 1)
+    DTri* emis = nullptr;             // last-bounce light probe: records of the emissive triangles
+    uint32_t num_emis = 0;            // (0 = probe off: spheres present, too many emitters, PT_NO_LIGHT_PROBE)
 };
 
 int pt::ctx_device(const pt_ctx* c) { return c->device; }
@@ -1732,6 +1788,20 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (!(sc->bvh[i].left & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].left] = i;
         if (!(sc->bvh[i].right & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].right] = i;
     }
+    // last-bounce light probe (shade_lane begin_trace): every triangle whose material has
+    // emission.r != 0 (the integrator's emission test, kernel.cu:453 -- not the caller's light list)
+    std::vector<DTri> em;
+    for (uint32_t i = 0; i < nt; ++i)
+        if (sc->mats[sc->tris[i].mat].emission[0] != 0) {
+            const DTri r = tri_rec(i);   // permuted for tri_hit_pk, as the render path's records
+            DTri q;
+            q.a = make_float4(r.a.x, r.a.y, r.a.w, r.b.x);
+            q.b = make_float4(r.b.z, r.b.w, r.a.z, r.b.y);
+            q.c = r.c;
+            em.push_back(q);
+        }
+    if (em.size() > kMaxProbeEmitters || sc->num_spheres > 0 || getenv("PT_NO_LIGHT_PROBE")) em.clear();
+    c->num_emis = (uint32_t)em.size();
     std::vector<DShade> sh(nt);
     for (uint32_t i = 0; i < nt; ++i) {
         sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
@@ -1803,7 +1873,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
         (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) ||
-        (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u)))) {
+        (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u))) ||
+        (rc = upload(&c->emis, em))) {
         pt_destroy(c);
         return bail(rc);
     }
@@ -1826,7 +1897,7 @@ void pt_destroy(pt_ctx* c)
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
-                    c->tone_thr, c->spheres, c->tri_counts};
+                    c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1858,6 +1929,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.num_lights = c->num_lights; a.total_light_area = c->total_light_area;
     a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;
     a.sphere_mat_base = c->sphere_mat_base;
+    a.emis = c->emis; a.num_emis = c->num_emis;
     memcpy(a.root, c->root, sizeof(a.root));
     a.cam.pos[0] = cam->pos.x; a.cam.pos[1] = cam->pos.y; a.cam.pos[2] = cam->pos.z;
     a.cam.dist = cam->dist_from_film; a.cam.focal = cam->focal_length; a.cam.radius = cam->radius;
@@ -1913,6 +1985,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.node_mask = c->node4_mask;
         b.top_nodes = c->top_nodes;
         const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
+                              kProbeLdsBytes +
                               (size_t)b.top_nodes * kTopNodeBytes;
         uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
         // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
