@@ -170,6 +170,59 @@ def roofline(counts, kms, W, H, args, world):
     return roof
 
 
+class FrameLoop:
+    """Frames rendered back to back into a ring of framebuffers, each frame's reduce to rank 0
+    issued asynchronously so that it overlaps the next frame's render (a buffer is zeroed again
+    only after its reduce has completed -- `wait()` orders the stream, the host does not block).
+
+    render(buf) -> stats dict: renders this rank's tiles into the zero-filled buf.
+    reduce(buf) -> work with .wait(), or None (one process, or a synchronous reduce).
+    Every frame is rendered and reduced in full; `drain()` returns the last frame's buffer once its
+    reduce is ordered before whatever the caller does next."""
+
+    def __init__(self, bufs, render, reduce=None):
+        self.bufs = list(bufs)
+        self.render = render
+        self.reduce = reduce
+        self.pending = [None] * len(self.bufs)
+        self.frames = 0
+
+    def step(self):
+        k = self.frames % len(self.bufs)
+        if self.pending[k] is not None:
+            self.pending[k].wait()
+            self.pending[k] = None
+        buf = self.bufs[k]
+        buf.zero_()
+        st = self.render(buf)
+        if self.reduce is not None:
+            self.pending[k] = self.reduce(buf)
+        self.frames += 1
+        return st
+
+    def drain(self):
+        for k, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[k] = None
+        return self.bufs[(self.frames - 1) % len(self.bufs)] if self.frames else self.bufs[0]
+
+
+def make_reduce(dist, backend, rank):
+    """RCCL (backend nccl): an async reduce(SUM) to rank 0 on the device tensor.  gloo (rehearsal of
+    the multi-process path on one GPU or on CPU): a synchronous reduce through host memory."""
+    if backend == "nccl":
+        return lambda buf: dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+
+    def gloo_reduce(buf):
+        host = buf.cpu() if buf.is_cuda else buf
+        dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+        if rank == 0 and host is not buf:
+            buf.copy_(host)
+        return None
+    return gloo_reduce
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,9 +256,18 @@ def main():
     if world != args.gpus:
         log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
     distributed = world > 1
+    # PT_BENCH_BACKEND=gloo rehearses the multi-process path where RCCL cannot run (several ranks
+    # on one GPU: the device index wraps over the visible GPUs when there are fewer than ranks)
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:
+        local = local % ndev
     torch.cuda.set_device(local)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     os.makedirs(args.cache_dir, exist_ok=True)
     path, mtl, scene_name = scene_path(args.cache_dir)
@@ -214,26 +276,24 @@ def main():
     W, H = args.width, args.height
     cam = pt.make_camera(width=W, height=H, **cam_kw)
     r = pt.Renderer(scene, device=local)
-    fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    # two framebuffers: frame k's RCCL reduce runs while frame k+1 renders into the other one
+    fbs = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(2 if distributed else 1)]
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step():
-        fb.zero_()
-        st = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
-                             flags=args.flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
-        if distributed:
-            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-        return st
+    def render(buf, flags=0):
+        return r.render_device(cam, buf.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
+                               flags=args.flags | flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
+
+    loop = FrameLoop(fbs, render, make_reduce(dist, backend, rank) if distributed else None)
 
     # counting pass (same inputs, counting variant): algorithmic bytes of the render kernel
     counts = None
     if not args.no_count:
-        fb.zero_()
-        counts = r.render_device(cam, fb.data_ptr(), W, H, args.spp, bounces=args.bounces,
-                                 integrator=args.integrator, flags=args.flags | pt.PT_FLAG_COUNT,
-                                 shard_index=rank, shard_count=shards, stream_ptr=stream)
+        fbs[0].zero_()
+        counts = render(fbs[0], pt.PT_FLAG_COUNT)
     for _ in range(args.warmup):
-        step()
+        loop.step()
+    loop.drain()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -241,16 +301,18 @@ def main():
     kernel_ms = []
     stats = []
     for _ in range(args.steps):
-        st = step()
+        st = loop.step()
         kernel_ms.append(st["kernel_ms"])
         stats.append(st)
+    fb = loop.drain()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    dev = "cuda" if backend == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     tot = torch.tensor([sum(s["samples"] for s in stats), sum(s["rays_traced"] for s in stats),
-                        sum(s["rays_reference"] for s in stats)], dtype=torch.float64, device="cuda")
+                        sum(s["rays_reference"] for s in stats)], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
