@@ -71,6 +71,8 @@ struct Args {
     uint32_t nmid;                  // into chunks_mid sample chunks, the rest into `chunks`; units are
     uint32_t chunks_mid;            // numbered whole, then mid (chunk-major), then the rest (chunk-major)
     uint32_t chunks;                // (init_pixel_states writes each unit's pixel and sample range)
+    uint32_t nfin;                  // ... of which the last nfin slots form a third grade of chunks_fin
+    uint32_t chunks_fin;            // chunks (the queue's final, shortest units)
     uint32_t* pmemo;                // split slots: primary hit of tail slot t as one 64-bit word: lo = tri + 2
                                     // (0 = not yet), hi = t
     double* lbuf;                   // split slots: per-sample radiance, channel k of sample n of tail slot t
@@ -82,6 +84,8 @@ struct Args {
     uint32_t* tri_counts;           // PT_FLAG_COUNT: per-triangle test counts by original id (kernel.cu:133)
     const DTri* emis;               // last-bounce light probe: the emissive triangles' records (see begin_trace)
     uint32_t num_emis;              // 0 = probe off
+    unsigned long long* lane_times; // diagnostic (PT_LANE_TIMING): wall clock of each lane's end, then each
+                                    // wave's start and exit (render_unidir_wf), or null
 };
 
 __device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
@@ -665,11 +669,15 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     const bool split = q >= a.nwhole;
     const uint32_t t = q - a.nwhole;   // split slot (row of the per-sample buffer)
     const bool mid = split && t < a.nmid;
-    const uint32_t nc = !split ? 1u : mid ? a.chunks_mid : a.chunks;
+    const uint32_t f0 = a.ntail - a.nfin;   // first slot of the final grade
+    const bool fin = split && t >= f0;
+    const uint32_t nc = !split ? 1u : mid ? a.chunks_mid : fin ? a.chunks_fin : a.chunks;
     auto unit = [&](uint32_t c) -> size_t {
         if (!split) return (size_t)q;
         if (mid) return (size_t)a.nwhole + (size_t)c * a.nmid + t;
-        return (size_t)a.nwhole + (size_t)a.chunks_mid * a.nmid + (size_t)c * (a.ntail - a.nmid) + (t - a.nmid);
+        const size_t fine0 = (size_t)a.nwhole + (size_t)a.chunks_mid * a.nmid;
+        if (!fin) return fine0 + (size_t)c * (f0 - a.nmid) + (t - a.nmid);
+        return fine0 + (size_t)a.chunks * (f0 - a.nmid) + (size_t)c * a.nfin + (t - f0);
     };
     const size_t N = a.nunits;
     uint32_t px, py;
@@ -745,6 +753,14 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 enum : int { SEC_PASS = 0, SEC_CHECK, SEC_SLOW, SEC_BOUNCE, SEC_EMIT, SEC_COSINE, SEC_LIGHT, SEC_SAMPLE_END,
              SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, SEC_PROBE, kSections = 16 };
 constexpr int kHist = 16;   // counting variant: walk steps per ray, log2 buckets (counters[48 + b])
+constexpr int kCounterWords = 96;   // counters[]: 0..63 as listed, 64..95 the tail bins
+constexpr int kTailBins = 16;   // counting variant: lane end / wave exit times after the queue drained,
+                                // bin k = [10 us x 2^(k-1), 10 us x 2^k) of the 100-MHz wall clock (bin 0: < 10 us)
+__device__ __forceinline__ uint32_t tail_bin(unsigned long long ticks)
+{
+    const unsigned long long q = ticks / 1000ull;
+    return q == 0ull ? 0u : min((uint32_t)kTailBins - 1, 64u - (uint32_t)__clzll((long long)q));
+}
 #ifdef PT_SEC_MARKERS   // analysis builds: mark the sections in the ISA listing
 #define SEC_MARK(k) asm volatile("; SEC " #k)
 #else
@@ -775,7 +791,7 @@ __device__ __forceinline__ const Args& kernel_args_opaque()
 template <bool kCount>
 __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
                                            int32_t& htri, float& ht, W4& w, const Stack4& S,
-                                           unsigned long long* lcnt, const uint32_t* lprobe)
+                                           unsigned long long* lcnt, const uint32_t* lprobe, uint32_t* done_rel)
 {
     (void)a_in;
     const Args& a = kernel_args_opaque();
@@ -1096,7 +1112,15 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
         if (state == ST_IDLE) {
             const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             if (u >= a.nunits) {
-                if (kCount) atomicMin(a.counters + 21, (unsigned long long)wall_clock64());   // queue drained
+                if (kCount) {   // queue drained; this lane's end after it and since the start (binned at the end)
+                    const unsigned long long now = wall_clock64();
+                    atomicMin(a.counters + 21, now);
+                    const unsigned long long d0 = __hip_atomic_load(a.counters + 21, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long s0 = __hip_atomic_load(a.counters + 20, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    done_rel[0] = (uint32_t)min(now - min(now, d0), 0xffffffffull);
+                    done_rel[1] = (uint32_t)min(now - min(now, s0), 0xffffffffull);
+                }
+                if (a.lane_times) a.lane_times[R.voff >> 4] = wall_clock64();
                 state = ST_DONE;
             } else {
                 // the unit as init_pixel_states prepared it (pixel, sample range, curand_init's
@@ -1158,6 +1182,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     uint32_t start_wait = 0;                    // counting variant: lanes without a ray when a walk phase starts
     uint32_t itc[6] = {0, 0, 0, 0, 0, 0};       // counting variant: walk-iteration classes (counters[14..19])
     unsigned long long walk_clk = 0, shade_clk = 0;   // counting variant: wave-clock per phase
+    uint32_t done_rel[2] = {0, 0};                    // counting variant: ticks from the queue's drain / the
+                                                      // kernel's start to this lane's end
 
     // hot state: what the walk phase needs
     uint32_t state = ST_IDLE;
@@ -1189,6 +1215,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.top = reinterpret_cast<const char*>(ltop);
     S.ntop = a.top_nodes;
     __syncthreads();
+    const uint32_t nlanes = gridDim.x * blockDim.x, wave_id = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (a.lane_times && lane == 0) a.lane_times[nlanes + wave_id] = wall_clock64();
 
     for (;;) {
         // ---------------------------------------------------------------- walk
@@ -1241,18 +1269,30 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (kCount) ++shade_slots;
         // (the lane id is recomputed for the shading pass: one VGPR less live across the walk loop)
         if (state != ST_TRACE && state != ST_DONE)
-            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe);
+            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
+    if (a.lane_times && lane == 0) a.lane_times[nlanes + nlanes / 64 + wave_id] = wall_clock64();
     if (kCount) {
         if (lane == 0) { atomicAdd(a.counters + 9, walk_clk); atomicAdd(a.counters + 10, shade_clk); }
-        if (lane == 0) {   // wave exit times (wall clock): last, and the sum for the mean
+        if (lane == 0) {   // wave exit times (wall clock): last, the sum for the mean, and after the drain
             const unsigned long long t = wall_clock64();
             atomicMax(a.counters + 22, t);
             atomicAdd(a.counters + 23, t);
             atomicAdd(a.counters + 24, 1ull);
+            const unsigned long long d0 = __hip_atomic_load(a.counters + 21, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(a.counters + 80 + tail_bin(t - min(t, d0)), 1ull);
         }
+        // lane ends after the drain (log2 bins: one atomic per occupied bin and wave), and their sum
+        // since the kernel's start (the tail's idle lane-time = lanes x last exit - that sum)
+        const uint32_t bin = tail_bin(done_rel[0]);
+        for (uint32_t k = 0; k < (uint32_t)kTailBins; ++k) {
+            const uint64_t m = __ballot(bin == k);
+            if (m && lane == 0) atomicAdd(a.counters + 64 + k, (unsigned long long)__popcll(m));
+        }
+        const unsigned long long dsum = wave_sum(done_rel[1]);
+        if (lane == 0) atomicAdd(a.counters + 26, dsum);
         const unsigned long long c2 = wave_sum(cnt.nodes), c3v = wave_sum(cnt.tris), c5 = wave_sum(walk_slots);
         const unsigned long long c13 = wave_sum(cnt.top), c25 = wave_sum(cnt.spills);
         const unsigned long long c6 = wave_sum(cnt.leaf_steps), c7 = wave_sum(shade_slots);
@@ -1477,6 +1517,8 @@ struct pt_ctx {
                                     // -1 = automatic, 0 or 1 = one split for all)
     double wf_fine_px = 0.5;        // ... the last pixels per resident lane (PT_WF_FINE_PX)
     int wf_fine_chunks = 0;         // ... and their chunks (PT_WF_FINE_CHUNKS; 0 = the automatic count)
+    double wf_fin_px = 0.0;         // final grade: the last pixels per resident lane (PT_WF_FIN_PX) ...
+    int wf_fin_chunks = 0;          // ... in this many chunks (PT_WF_FIN_CHUNKS; <= the fine count = off)
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
     uint32_t wf_top = kTopNodesMax; // BVH4 nodes staged in each block's LDS (PT_WF_TOP; 0 = none)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
@@ -1690,6 +1732,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_MID_CHUNKS")) c->wf_mid_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_FINE_PX")) c->wf_fine_px = std::max(0.0, atof(e));
         if (const char* e = getenv("PT_WF_FINE_CHUNKS")) c->wf_fine_chunks = atoi(e);
+        if (const char* e = getenv("PT_WF_FIN_PX")) c->wf_fin_px = std::max(0.0, atof(e));
+        if (const char* e = getenv("PT_WF_FIN_CHUNKS")) c->wf_fin_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_ITERS")) c->wf_iters = (uint32_t)std::max(1, atoi(e));
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
     }
@@ -1878,7 +1922,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         pt_destroy(c);
         return bail(rc);
     }
-    if (hipMalloc(reinterpret_cast<void**>(&c->counters), 64 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void**>(&c->counters), kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), 16) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -1903,6 +1947,35 @@ void pt_destroy(pt_ctx* c)
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
+}
+
+// PT_LANE_TIMING summary of one wavefront render: wall-clock ticks (100 MHz) from the first wave's start
+// to the queue's drain (the first lane without a unit), to the mean and the last lane end, and to the
+// last wave exit; idle = the lane-time after each lane's end, as a fraction of lanes x kernel span.
+static void write_lane_timing(const char* path, const std::vector<unsigned long long>& t, size_t lanes, int shards)
+{
+    const size_t waves = lanes / 64;
+    unsigned long long t0 = ~0ull, drain = ~0ull, lend = 0, wexit = 0;
+    for (size_t w = 0; w < waves; ++w) {
+        if (t[lanes + w]) t0 = std::min(t0, t[lanes + w]);
+        wexit = std::max(wexit, t[lanes + waves + w]);
+    }
+    double sum = 0.0;
+    size_t n = 0;
+    for (size_t l = 0; l < lanes; ++l) {
+        if (!t[l]) continue;
+        drain = std::min(drain, t[l]);
+        lend = std::max(lend, t[l]);
+        sum += (double)(t[l] - t0);
+        ++n;
+    }
+    if (!n || t0 == ~0ull) return;
+    const double span = (double)(wexit - t0);
+    if (FILE* f = fopen(path, "a")) {
+        fprintf(f, "lane_timing shards %d lanes %zu span %.0f drain %.0f mean_end %.0f last_end %.0f idle_frac %.4f\n", shards,
+                n, span, (double)(drain - t0), sum / (double)n, (double)(lend - t0), 1.0 - (sum / (double)n) / span);
+        fclose(f);
+    }
 }
 
 int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* d_out, void* stream_v, pt_stats* st)
@@ -1965,7 +2038,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam &&
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 64 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, kCounterWords * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
     if (count && (p->flags & PT_FLAG_TRI_COUNTS)) {   // per-triangle test counts of this render (pt_tri_counts)
         HIP_TRY(hipMemsetAsync(c->tri_counts, 0, (size_t)std::max<uint32_t>(c->num_tris, 1u) * 4, stream));
@@ -2044,15 +2117,26 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 ntail = (uint32_t)cap;
             }
         }
-        if ((uint64_t)b.npix + (uint64_t)ntail * (std::max(chunks, chunks_mid) - 1) > 0xffffffffull) chunks = 1;
+        // final grade: the queue's last units shorter still (the kernel ends when the units started
+        // last are done), carved from the end of the fine grade
+        uint32_t nfin = 0, chunks_fin = 1;
+        if (ntail > nmid && c->wf_fin_px > 0.0 && c->wf_fin_chunks > (int)chunks) {
+            nfin = (uint32_t)std::min<uint64_t>(ntail - nmid, (uint64_t)(c->wf_fin_px * (double)lanes));
+            chunks_fin = (uint32_t)std::min(c->wf_fin_chunks, p->spp);
+        }
+        if ((uint64_t)b.npix + (uint64_t)ntail * (std::max(std::max(chunks, chunks_mid), chunks_fin) - 1) > 0xffffffffull)
+            chunks = 1;
         if (chunks <= 1 || ntail == 0) { chunks = 1; ntail = 0; nmid = 0; }
         if (nmid == 0) chunks_mid = 1;
+        if (ntail == 0 || chunks_fin <= chunks) { nfin = 0; chunks_fin = 1; }
         b.chunks = chunks;
         b.ntail = ntail;
         b.nmid = nmid;
         b.chunks_mid = chunks_mid;
+        b.nfin = nfin;
+        b.chunks_fin = chunks_fin;
         b.nwhole = b.npix - ntail;
-        b.nunits = b.nwhole + nmid * chunks_mid + (ntail - nmid) * chunks;
+        b.nunits = b.nwhole + nmid * chunks_mid + (ntail - nmid - nfin) * chunks + nfin * chunks_fin;
         const uint32_t need = (b.nunits + paths_per_block - 1) / paths_per_block;
         if (blocks > need) blocks = need;
         if (ntail > 0) {
@@ -2092,6 +2176,16 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             c->pix_states_words = sw;
         }
         b.pix_states = c->pix_states;
+        // diagnostic: per-lane end / per-wave start and exit times (PT_LANE_TIMING=file appends a summary)
+        const char* timing_path = getenv("PT_LANE_TIMING");
+        std::vector<unsigned long long> times;
+        unsigned long long* d_times = nullptr;
+        if (timing_path) {
+            times.assign((size_t)blocks * 256 + 2 * (size_t)blocks * 4, 0ull);
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_times), times.size() * 8));
+            HIP_TRY(hipMemsetAsync(d_times, 0, times.size() * 8, stream));
+            b.lane_times = d_times;
+        }
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
         if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
@@ -2101,6 +2195,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         HIP_TRY(hipGetLastError());
         if (b.ntail > 0) hipLaunchKernelGGL(finalize_pixels, dim3((b.ntail + 255) / 256), dim3(256), 0, stream, b);
         HIP_TRY(hipGetLastError());
+        if (d_times) {
+            HIP_TRY(hipMemcpyAsync(times.data(), d_times, times.size() * 8, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            (void)hipFree(d_times);
+            write_lane_timing(timing_path, times, (size_t)blocks * 256, p->shard_count);
+        }
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
         if (p->integrator == PT_INTEGRATOR_HEAD) {
@@ -2114,7 +2214,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev1, stream));
-    unsigned long long cnt[64];
+    unsigned long long cnt[kCounterWords];
     HIP_TRY(hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     if (count) {
@@ -2128,7 +2228,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                         cnt[2], cnt[6], cnt[12], cnt[13]);
                 fprintf(f, "wall_clock start %llu drained %llu last_exit %llu mean_exit %.1f waves %llu (ticks)\n", cnt[20], cnt[21],
                         cnt[22], cnt[24] ? (double)cnt[23] / (double)cnt[24] : 0.0, cnt[24]);
-                fprintf(f, "iters_by_deep_lanes 0:%llu 1-4:%llu 5-8:%llu more:%llu no_leaf %llu neither %llu\n", cnt[14],
+                fprintf(f, "lane_end_mean %.1f (ticks since start)\ntail_lane_end_log2_10us",
+                        cnt[24] ? (double)cnt[26] / (64.0 * (double)cnt[24]) : 0.0);
+                for (int k = 0; k < kTailBins; ++k) fprintf(f, " %llu", cnt[64 + k]);
+                fprintf(f, "\ntail_wave_exit_log2_10us");
+                for (int k = 0; k < kTailBins; ++k) fprintf(f, " %llu", cnt[80 + k]);
+                fprintf(f, "\niters_by_deep_lanes 0:%llu 1-4:%llu 5-8:%llu more:%llu no_leaf %llu neither %llu\n", cnt[14],
                         cnt[15], cnt[16], cnt[17], cnt[18], cnt[19]);
                 fclose(f);
             }
@@ -2256,7 +2361,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_tri), (size_t)n * 4));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_t), (size_t)n * 4));
         HIP_TRY(hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemset(c->counters, 0, 64 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(c->counters, 0, kCounterWords * sizeof(unsigned long long)));
         const bool count = tri_counts != nullptr || spill_entries != nullptr;
         if (tri_counts && c->num_tris > 0) {
             HIP_TRY(hipMemset(c->tri_counts, 0, (size_t)c->num_tris * 4));

@@ -195,6 +195,28 @@ def test_two_level_split_units_bit_exact(oracle_mod, monkeypatch, mid, fine_px, 
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("mid,fine_px,fine,fin_px,fin,radius", [("2", "0.0003", "4", "0.0001", "9", 0.0),
+                                                              ("3", "0.0005", "3", "0.0002", "5", 0.05),
+                                                              ("0", "0", "3", "0.0003", "7", 0.0)])
+def test_three_grade_split_units_bit_exact(oracle_mod, monkeypatch, mid, fine_px, fine, fin_px, fin, radius):
+    """A third, final grade of split units (PT_WF_FIN_PX / PT_WF_FIN_CHUNKS: the queue's last
+    pixels in the most chunks, down to one sample per unit): the same image bits as the oracle."""
+    monkeypatch.setenv("PT_WF_MID_CHUNKS", mid)
+    monkeypatch.setenv("PT_WF_FINE_PX", fine_px)
+    monkeypatch.setenv("PT_WF_FINE_CHUNKS", fine)
+    monkeypatch.setenv("PT_WF_FIN_PX", fin_px)
+    monkeypatch.setenv("PT_WF_FIN_CHUNKS", fin)
+    s = load_scene("cornell_blob")
+    w, h, spp = 24, 16, 9
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=3)
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 0, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+
+
 def test_rmse_and_properties_larger(oracle_mod, cb):
     """North-star tolerance on a subset of a larger render (oracle only on the subset)."""
     s, r = cb
