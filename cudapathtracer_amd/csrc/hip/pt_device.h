@@ -495,7 +495,7 @@ struct W4 {
     V3 inv;              // RN(1/d): also the Markstein reciprocal for the exact checks
     V3 oi;               // o * inv, for the conservative box test t = fma(b, inv, -oi)
     uint32_t node;       // next node to visit, kNone = pop one
-    uint32_t leaf;       // leaves to test: (first slot << 4) | mask of entered leaf children; none
+    uint32_t leaf;       // leaves to test: (first slot << 8) | mask of the entered leaves' slots; none
                          // pending when the mask is 0 (leaf4_pending)
     int32_t sp;          // node stack depth
     int32_t lsp;         // leaf entries queued in the LDS leaf ring (besides `leaf`)
@@ -524,14 +524,17 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
     }
 }
 
-__device__ __forceinline__ bool leaf4_pending(const W4& w) { return (w.leaf & 15u) != 0u; }
+// leaf queue entry: (the node's first leaf slot << kLeafBits) | mask of the entered leaves' slots
+// (a node's leaf children hold at most kLeafBits triangles; slots < 2^(31 - kLeafBits))
+constexpr uint32_t kLeafBits = 8;
+__device__ __forceinline__ bool leaf4_pending(const W4& w) { return (w.leaf & ((1u << kLeafBits) - 1u)) != 0u; }
 // the pending entry's lowest entered leaf slot (the mask is the low 4 bits: the word's lowest set
 // bit); an opaque v_ffbl so that the compiler recomputes it instead of keeping it live
 __device__ __forceinline__ uint32_t leaf4_slot(const W4& w)
 {
     uint32_t b;
     asm volatile("v_ffbl_b32 %0, %1" : "=v"(b) : "v"(w.leaf));
-    return (w.leaf >> 4) + b;
+    return (w.leaf >> kLeafBits) + b;
 }
 
 // walk4_begin in two halves: the ray-independent reset, and the per-ray reciprocals / plane
@@ -776,13 +779,18 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
                    lim, t2, t3, e2, e3);
         uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
-        // entered leaf children as one queue entry: their slots are consecutive from child 0's
-        // (leaf children come first), so the entry is child 0's slot and a 4-bit mask
+        // entered leaf children as one queue entry: the node's leaf triangles have consecutive
+        // slots from its first (leaf children come first; each leaf child's word carries its slot
+        // bits), so the entry is that slot and an 8-bit mask
         // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
         const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
-        const uint32_t lm = (e0 && l0 ? 1u : 0u) | (e1 && l1 ? 2u : 0u) | (e2 && l2 ? 4u : 0u) | (e3 && l3 ? 8u : 0u);
+        constexpr uint32_t kB = 31 - kLeafBits;   // a leaf child's word: kLeaf | slot bits << kB | first slot
+        const uint32_t lm = (e0 && l0 ? __builtin_amdgcn_ubfe(r0, kB, kLeafBits) : 0u) |
+                            (e1 && l1 ? __builtin_amdgcn_ubfe(r1, kB, kLeafBits) : 0u) |
+                            (e2 && l2 ? __builtin_amdgcn_ubfe(r2, kB, kLeafBits) : 0u) |
+                            (e3 && l3 ? __builtin_amdgcn_ubfe(r3, kB, kLeafBits) : 0u);
         if (lm != 0u) {
-            const uint32_t e = (r0 << 4) | lm;   // (the kLeaf bit shifts out)
+            const uint32_t e = (__builtin_amdgcn_ubfe(r0, 0, kB) << kLeafBits) | lm;
             if (!leaf4_pending(w)) w.leaf = e;
             else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
         }

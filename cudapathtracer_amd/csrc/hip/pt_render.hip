@@ -1782,9 +1782,11 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         }
         c->top_nodes = std::min(std::max(c->wf_top, 1u), n4);   // (>= 1: the wavefront walk reads the LDS top unconditionally)
         an.resize(n4);
-        // Triangle slots: the leaf children of each node (in node order) get consecutive slots, and
-        // each node lists its leaf children first -- the walk queues a node's entered leaves as one
-        // entry (first slot, 4-bit mask).  slot_leaf[s] = the binary BVH's leaf slot.
+        // Triangle slots: the triangles of each node's leaf children (in node order) get consecutive
+        // slots, and each node lists its leaf children first -- the walk queues a node's entered
+        // leaves as one entry (first slot, 8-bit mask of slots).  A leaf child's word is
+        // kLeaf | its slot bits relative to the node's first slot << 23 | that first slot.
+        // slot_leaf[s] = the binary BVH's leaf slot (one triangle) of render slot s.
         std::vector<uint32_t> slot_leaf;
         slot_leaf.reserve(nt);
         for (size_t i = 0; i < n4; ++i) {
@@ -1793,13 +1795,20 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             int order[4], m = 0;
             for (int k = 0; k < 4; ++k) if (is_leaf(x0.child[k])) order[m++] = k;
             for (int k = 0; k < 4; ++k) if (!is_leaf(x0.child[k])) order[m++] = k;
+            const uint32_t base = (uint32_t)slot_leaf.size();
             for (int k = 0; k < 4; ++k) {
                 const int q = order[k];
                 for (int ax = 0; ax < 3; ++ax) { x.lo[ax][k] = x0.lo[ax][q]; x.hi[ax][k] = x0.hi[ax][q]; }
                 x.child[k] = x0.child[q];
                 if (is_leaf(x.child[k])) {
-                    slot_leaf.push_back(x.child[k] ^ PT_BVH_LEAF_FLAG);
-                    x.child[k] = PT_BVH_LEAF_FLAG | (uint32_t)(slot_leaf.size() - 1);
+                    const uint32_t first = (uint32_t)slot_leaf.size() - base, cnt = pt::accel_leaf_count(x.child[k]);
+                    for (uint32_t j = 0; j < cnt; ++j) slot_leaf.push_back(pt::accel_leaf_slot(x.child[k]) + j);
+                    static_assert(pt::kAccel4LeafTris <= kLeafBits, "leaf slot mask width");
+                    if (first + cnt > kLeafBits || base >= (1u << (31 - kLeafBits))) {
+                        delete c;
+                        return bail(pt::fail(PT_E_SCENE, "pt_create: %u triangles exceed the render path's leaf slot range", nt));
+                    }
+                    x.child[k] = PT_BVH_LEAF_FLAG | ((((1u << cnt) - 1u) << first) << (31 - kLeafBits)) | base;
                 }
             }
             for (int k = 0; k < 4; ++k)

@@ -41,9 +41,17 @@ struct Builder {
     AccelBvh& out;
     float margin;
     int max_depth = 0;
+    // Leaves of up to 2 triangles where the SAH favours them (measured on C3: 7% fewer BVH4 node
+    // visits for 16% more triangle tests, +3% Msamples/s; 3 or 4 gain nothing more)
+    size_t leaf_max = kAccelLeafMax;   // largest leaf (triangles; PT_LEAF_MAX)
+    float node_cost = 1.0f;            // SAH cost of a binary node visit, in triangle tests (PT_LEAF_NODE_COST)
 
     Builder(const std::vector<TriBox>& t, std::vector<uint32_t>& it, AccelBvh& o, float m)
-        : tb(t), items(it), out(o), margin(m) {}
+        : tb(t), items(it), out(o), margin(m)
+    {
+        if (const char* v = getenv("PT_LEAF_MAX")) leaf_max = std::min<size_t>(kAccelLeafMax, std::max(1, atoi(v)));
+        if (const char* v = getenv("PT_LEAF_NODE_COST")) node_cost = (float)atof(v);
+    }
 
     void bounds(size_t b, size_t e, float* lo, float* hi) const
     {
@@ -128,15 +136,30 @@ struct Builder {
 
     // Returns the child reference of the subtree over items[b, e); nodes in preorder, leaf
     // slots in left-first DFS order.
+    uint32_t leaf(size_t b, size_t e)
+    {
+        const uint32_t slot = static_cast<uint32_t>(out.leaf_order.size());
+        for (size_t i = b; i < e; ++i) out.leaf_order.push_back(items[i]);
+        return PT_BVH_LEAF_FLAG | (static_cast<uint32_t>(e - b - 1) << 29) | slot;
+    }
+
     uint32_t build(size_t b, size_t e, int depth)
     {
         max_depth = std::max(max_depth, depth);
-        if (e - b == 1) {
-            const uint32_t slot = static_cast<uint32_t>(out.leaf_order.size());
-            out.leaf_order.push_back(items[b]);
-            return PT_BVH_LEAF_FLAG | slot;
-        }
+        if (e - b == 1) return leaf(b, e);
         const size_t mid = split(b, e);
+        // a leaf of up to leaf_max triangles when its SAH cost (one test per triangle) is no more
+        // than the split's: node_cost + (n_L A_L + n_R A_R) / A
+        if (e - b <= leaf_max) {
+            float lo[3], hi[3], llo[3], lhi[3], rlo[3], rhi[3];
+            bounds(b, e, lo, hi);
+            bounds(b, mid, llo, lhi);
+            bounds(mid, e, rlo, rhi);
+            const float a = surface(lo, hi);
+            const float split_cost = node_cost + (a > 0.0f ? ((mid - b) * surface(llo, lhi) + (e - mid) * surface(rlo, rhi)) / a
+                                                            : (float)(e - b));
+            if ((float)(e - b) <= split_cost) return leaf(b, e);
+        }
         const uint32_t me = static_cast<uint32_t>(out.nodes.size());
         out.nodes.emplace_back();
         float box[2][6];
@@ -196,9 +219,7 @@ struct ParallelBuild {
         if (s.left < 0) {
             const uint32_t no = static_cast<uint32_t>(out.nodes.size());
             const uint32_t lo = static_cast<uint32_t>(out.leaf_order.size());
-            auto remap = [&](uint32_t ref) {
-                return (ref & PT_BVH_LEAF_FLAG) ? (PT_BVH_LEAF_FLAG | ((ref ^ PT_BVH_LEAF_FLAG) + lo)) : ref + no;
-            };
+            auto remap = [&](uint32_t ref) { return (ref & PT_BVH_LEAF_FLAG) ? ref + lo : ref + no; };
             for (AccelNode nd : s.local.nodes) {
                 nd.child[0] = remap(nd.child[0]);
                 nd.child[1] = remap(nd.child[1]);
@@ -313,11 +334,17 @@ struct Collapser {
             c[k].ref = bin.nodes[b].child[k];
             memcpy(c[k].box, bin.nodes[b].box[k], sizeof(c[k].box));
         }
+        // triangles in the leaf children (the walk queues a node's entered leaf triangles as one
+        // entry with a kAccel4LeafTris-bit slot mask)
+        auto leaf_tris = [](uint32_t ref) { return (ref & PT_BVH_LEAF_FLAG) ? accel_leaf_count(ref) : 0u; };
+        uint32_t tris = leaf_tris(c[0].ref) + leaf_tris(c[1].ref);
         while (n < 4) {   // expand the inner candidate with the largest surface area
             int pick = -1;
             float best = -1.0f;
             for (int k = 0; k < n; ++k) {
                 if (c[k].ref & PT_BVH_LEAF_FLAG) continue;
+                const AccelNode& y = bin.nodes[c[k].ref];
+                if (tris + leaf_tris(y.child[0]) + leaf_tris(y.child[1]) > kAccel4LeafTris) continue;
                 const float a = area_of(c[k].box);
                 if (a > best) { best = a; pick = k; }
             }
@@ -329,6 +356,7 @@ struct Collapser {
             c[pick].ref = x.child[0];
             memcpy(c[pick].box, x.box[0], sizeof(c[pick].box));
             c[n++] = second;
+            tris += leaf_tris(x.child[0]) + leaf_tris(x.child[1]);
         }
         const uint32_t me = static_cast<uint32_t>(out.nodes.size());
         out.nodes.emplace_back();

@@ -76,8 +76,12 @@ unsigned host_threads();
 // ---- render-path acceleration structure (accel_build.cpp) --------------------------------
 struct AccelNode {
     float box[2][6];       // child boxes (lo xyz, hi xyz), inflated by `margin`
-    uint32_t child[2];     // inner node index, or PT_BVH_LEAF_FLAG | leaf slot
+    uint32_t child[2];     // inner node index, or a leaf: PT_BVH_LEAF_FLAG | (count - 1) << 29 | first slot
 };
+// a leaf of the render-path BVH holds 1..kAccelLeafMax triangles at consecutive leaf slots
+constexpr uint32_t kAccelLeafMax = 2;
+inline uint32_t accel_leaf_count(uint32_t ref) { return ((ref >> 29) & 3u) + 1u; }
+inline uint32_t accel_leaf_slot(uint32_t ref) { return ref & 0x1fffffffu; }
 struct AccelBvh {
     std::vector<AccelNode> nodes;        // node 0 = root
     std::vector<uint32_t> leaf_order;    // triangle id of each leaf slot
@@ -86,12 +90,14 @@ struct AccelBvh {
     float margin = 0.0f;
 };
 int build_accel(const pt_scene& sc, AccelBvh* out);
-// SAH cost of the binary tree: the sum of its inner-node surface areas (one triangle per leaf)
+// SAH cost of the binary tree: the sum of its inner-node surface areas
 double accel_sah_cost(const AccelBvh& acc);
 
 // 4-wide collapse of the binary SAH BVH: each node holds up to 4 children (largest-area
-// expansion), empty slots are kAccel4Empty; leaves stay single triangles (same leaf slots).
+// expansion, at most kAccel4LeafTris triangles in its leaf children), empty slots are
+// kAccel4Empty; leaves keep their binary-BVH refs (count and first leaf slot).
 constexpr uint32_t kAccel4Empty = 0xffffffffu;
+constexpr uint32_t kAccel4LeafTris = 8;    // at most this many triangles in a node's leaf children (kLeafBits)
 struct Accel4Node {
     float lo[3][4], hi[3][4];   // [axis][child]
     uint32_t child[4];          // inner node index, PT_BVH_LEAF_FLAG | slot, or kAccel4Empty

@@ -16,6 +16,6 @@ for kv in ${SWEEP:--}; do
   env $envs PT_SECTION_DUMP=$PWD/$OUT/sections_$i.txt timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $cnt ${BENCH_ARGS} \
       > $OUT/b_$i.json 2> $OUT/b_$i.err || { echo "bench failed: $kv" > $OUT/done.txt; exit 1; }
   echo "$kv $(python3 -c "
-import json;d=json.load(open('$OUT/b_$i.json'));r=d['roofline'] or {};print(d['value'], d['ms_per_step'], r.get('walk_simd_util'), r.get('walk_phase_frac'), r.get('shade_phases'))")" >> $OUT/summary.txt
+import json;d=json.load(open('$OUT/b_$i.json'));r=d['roofline'] or {};print(d['value'], d['ms_per_step'], r.get('walk_simd_util'), r.get('walk_phase_frac'), r.get('shade_phases'), r.get('node_fetches'), r.get('tri_tests'))")" >> $OUT/summary.txt
 done
 echo ok > $OUT/done.txt
