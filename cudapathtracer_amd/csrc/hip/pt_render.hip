@@ -76,7 +76,8 @@ struct Args {
     uint32_t* pmemo;                // split slots: primary hit of tail slot t as one 64-bit word: lo = tri + 2
                                     // (0 = not yet), hi = t
     double* lbuf;                   // split slots: per-sample radiance, channel k of sample n of tail slot t
-                                    // at lbuf[(k * spp + n-1) * ntail + t]
+                                    // at lbuf[(t * spp + n-1) * 3 + k] (a slot's samples contiguous: each
+                                    // lane fills whole lines with its own consecutive samples)
     const float4* spheres;          // sphere primitives: center xyz, radius (hit ids num_tris + i)
     uint32_t num_spheres;
     uint32_t num_tris;
@@ -721,14 +722,13 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     uint32_t px, py;
     if (!unit_pixel(a, a.nwhole + t, &px, &py)) return;
     const size_t pix = (size_t)py * (size_t)a.w + px;
-    const size_t ch = (size_t)a.spp * a.ntail;   // channel stride
-    const double* L = a.lbuf + t;
+    const double* L = a.lbuf + (size_t)t * a.spp * 3;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-    for (int n = 1; n <= a.spp; ++n, L += a.ntail) {
+    for (int n = 1; n <= a.spp; ++n, L += 3) {
         const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
         m0 = (m0 * fn1) / fn + L[0] / fn;
-        m1 = (m1 * fn1) / fn + L[ch] / fn;
-        m2 = (m2 * fn1) / fn + L[2 * ch] / fn;
+        m1 = (m1 * fn1) / fn + L[1] / fn;
+        m2 = (m2 * fn1) / fn + L[2] / fn;
     }
     float* o3 = a.out + pix * 3;
     o3[0] = (float)m0;
@@ -1046,11 +1046,10 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     R.std_(CW_M, m0); R.st4(CW_M + 2, dlo(m1), dhi(m1), dlo(m2), dhi(m2));
                 } else {
                     // split pixel: keep L_n, finalize_pixels forms the ordered mean
-                    const size_t ch = (size_t)a.spp * a.ntail;
-                    double* L = a.lbuf + (size_t)(n - 1) * a.ntail + R.ld(CW_Q);
+                    double* L = a.lbuf + ((size_t)R.ld(CW_Q) * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
                     L[0] = acc.r;
-                    L[ch] = acc.g;
-                    L[2 * ch] = acc.b;
+                    L[1] = acc.g;
+                    L[2] = acc.b;
                     if ((uint32_t)n >= nend) {
                         state = ST_IDLE;
                         break;
