@@ -883,9 +883,12 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
     // dead after bounce 0) would otherwise run sample after sample here while the rest of the
     // wave waits; after wf_iters shading iterations it yields with its pending hit (ST_SHADE /
     // ST_SLOW) and resumes in the next pass, alongside the other lanes' work.
+    // The refill (lanes whose unit is finished take the next units of this shard) runs after the
+    // first shading iteration, so a unit that starts from a known first hit (a split pixel's memo)
+    // is shaded in the second iteration of the same pass instead of waiting out a walk phase.
     bool again = (state == ST_SHADE || state == ST_SLOW);
-    for (uint32_t iters = 0; again; ++iters) {
-        if (iters >= a.wf_iters) break;
+    for (uint32_t iters = 0; iters < a.wf_iters; ++iters) {
+      if (again) {
         again = false;
         if (state == ST_SLOW) {
             wave_count(lcnt + 3, lane);
@@ -1097,9 +1100,12 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
             again = begin_trace(ro, rd, bound);
             break;
         }
-    }
-
-    // refill: lanes whose pixel is finished take the next pixels of this shard
+      }
+      if (iters != 0u) {
+          if (__ballot(again) == 0ull) break;
+          continue;
+      }
+    // refill: lanes whose unit is finished take the next units of this shard
     const uint64_t idle = __ballot(state == ST_IDLE);
     if (idle) {
         SEC(SEC_REFILL);
@@ -1148,10 +1154,12 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     R.st2(CW_PX, px, py);
                     if (split && (fl & CF_LENS)) R.st(CW_Q, a.pix_states[UW_TQ * N + u]);
                     R.st2(CW_M, 0u, 0u); R.st4(CW_M + 2, 0u, 0u, 0u, 0u);
-                    start_sample(px, py);
+                    again = start_sample(px, py);
                 }
             }
         }
+    }
+      if (__ballot(again) == 0ull) break;
     }
 
     SEC(SEC_RECORD);
