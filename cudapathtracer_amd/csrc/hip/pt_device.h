@@ -784,13 +784,12 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         // bits), so the entry is that slot and an 8-bit mask
         // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
         const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
-        constexpr uint32_t kB = 31 - kLeafBits;   // a leaf child's word: kLeaf | slot bits << kB | first slot
-        const uint32_t lm = (e0 && l0 ? __builtin_amdgcn_ubfe(r0, kB, kLeafBits) : 0u) |
-                            (e1 && l1 ? __builtin_amdgcn_ubfe(r1, kB, kLeafBits) : 0u) |
-                            (e2 && l2 ? __builtin_amdgcn_ubfe(r2, kB, kLeafBits) : 0u) |
-                            (e3 && l3 ? __builtin_amdgcn_ubfe(r3, kB, kLeafBits) : 0u);
-        if (lm != 0u) {
-            const uint32_t e = (__builtin_amdgcn_ubfe(r0, 0, kB) << kLeafBits) | lm;
+        // a leaf child's word is kLeaf | first slot << kLeafBits | its slot bits, the first slot
+        // being the node's for all its leaf children: the OR of the entered leaf children's words
+        // is the queue entry (with kLeaf set)
+        const uint32_t lw = (e0 && l0 ? r0 : 0u) | (e1 && l1 ? r1 : 0u) | (e2 && l2 ? r2 : 0u) | (e3 && l3 ? r3 : 0u);
+        if ((lw & ((1u << kLeafBits) - 1u)) != 0u) {
+            const uint32_t e = lw & ~kLeaf;
             if (!leaf4_pending(w)) w.leaf = e;
             else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
         }

@@ -1793,7 +1793,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         // Triangle slots: the triangles of each node's leaf children (in node order) get consecutive
         // slots, and each node lists its leaf children first -- the walk queues a node's entered
         // leaves as one entry (first slot, 8-bit mask of slots).  A leaf child's word is
-        // kLeaf | its slot bits relative to the node's first slot << 23 | that first slot.
+        // kLeaf | the node's first leaf slot << kLeafBits | its slot bits relative to it.
         // slot_leaf[s] = the binary BVH's leaf slot (one triangle) of render slot s.
         std::vector<uint32_t> slot_leaf;
         slot_leaf.reserve(nt);
@@ -1816,7 +1816,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                         delete c;
                         return bail(pt::fail(PT_E_SCENE, "pt_create: %u triangles exceed the render path's leaf slot range", nt));
                     }
-                    x.child[k] = PT_BVH_LEAF_FLAG | ((((1u << cnt) - 1u) << first) << (31 - kLeafBits)) | base;
+                    x.child[k] = PT_BVH_LEAF_FLAG | (base << kLeafBits) | (((1u << cnt) - 1u) << first);
                 }
             }
             for (int k = 0; k < 4; ++k)
