@@ -644,6 +644,28 @@ __device__ __forceinline__ uint4 lds_u4(const char* base, uint32_t off)
     const u4v v = *(__attribute__((address_space(3))) const u4v*)(base + off);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// the same at a 32-bit LDS byte address (constant offsets added to it fold into the instruction)
+__device__ __forceinline__ uint32_t lds_addr(const char* p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ float4 lds_f4a(uint32_t a)
+{
+    const f4v v = *(__attribute__((address_space(3))) const f4v*)(uintptr_t)a;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 lds_u4a(uint32_t a)
+{
+    const u4v v = *(__attribute__((address_space(3))) const u4v*)(uintptr_t)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// a - b as one opaque v_sub (the compiler would otherwise form -b and add it)
+__device__ __forceinline__ uint32_t vsub_u32(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float4 glb_f4(const void* base, uint32_t off)
 {
     const f4v v = *(__attribute__((address_space(1))) const f4v*)(reinterpret_cast<const char*>(base) + off);
@@ -727,9 +749,11 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 1);
     const bool leaf = leaf4_pending(w);
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
-    const uint32_t tb = mul48(leaf ? leaf4_slot(w) : 0u);
-    float4 A = ld_f4(tris, tb), B = ld_f4(tris, tb + 16u);
-    float e2z = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tris) + tb + 32u);
+    // (slots < 2^23, see kLeafBits: a full-rate 24-bit multiply; the slot is formed unconditionally
+    // and selected, no branch)
+    const uint32_t tb = __umul24(leaf ? leaf4_slot(w) : 0u, (uint32_t)sizeof(DTri));
+    float4 A = glb_f4(tris, tb), B = glb_f4(reinterpret_cast<const char*>(tris) + 16, tb);
+    float e2z = *(__attribute__((address_space(1))) const float*)(reinterpret_cast<const char*>(tris) + 32 + tb);
     // a lane with no node to visit reads node 0 (the LDS copy when there is one)
     const uint32_t nidx = visit ? w.node : 0u;
     float4 NX, FX, NY, FY, NZ, FZ;
@@ -739,11 +763,14 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     // write the same registers and an LDS read issued behind outstanding global loads to them
     // would have to wait out their whole latency.
     if (kTop || S.ntop != 0u) {
-        const char* const lb = S.top + __umul24(nidx < S.ntop ? nidx : 0u, kTopNodeBytes);   // (full-rate multiply)
-        NX = lds_f4(lb, w.nx); FX = lds_f4(lb, w.nx ^ 48u);
-        NY = lds_f4(lb, w.ny); FY = lds_f4(lb, w.ny ^ 80u);
-        NZ = lds_f4(lb, w.nz); FZ = lds_f4(lb, w.nz ^ 112u);
-        ch = lds_u4(lb, 96u);
+        const uint32_t m = __umul24(nidx < S.ntop ? nidx : 0u, kTopNodeBytes);   // (full-rate multiply)
+        // far plane offsets: nx ^ 48 == 48 - nx for nx in {0, 48} (likewise 80 - ny, 112 - nz), so a
+        // far address is (m - near offset) with the constants (and the top's base) in the offset field
+        const uint32_t mb = lds_addr(S.top) + m;
+        NX = lds_f4a(mb + w.nx); FX = lds_f4a(vsub_u32(mb, w.nx) + 48u);
+        NY = lds_f4a(mb + w.ny); FY = lds_f4a(vsub_u32(mb, w.ny) + 80u);
+        NZ = lds_f4a(mb + w.nz); FZ = lds_f4a(vsub_u32(mb, w.nz) + 112u);
+        ch = lds_u4a(mb + 96u);
     }
     if (nidx >= S.ntop) {
         const uint32_t nb = nidx * 128u;

@@ -539,7 +539,8 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
 // direction, finishes samples / pixels and fetches new pixels.  Lanes therefore do not idle
 // until the slowest ray of the wave is done, which is where the tile kernel loses most time.
 // Arithmetic and RNG consumption per lane are exactly those of radianceAlongSingleStep2.
-enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4, ST_CHECK = 5 };
+enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2, ST_DONE = 3, ST_SLOW = 4, ST_CHECK = 5,
+                  ST_WALKED = 6 };   // (walk finished in this walk phase: CHECK / SHADE / SLOW decided after it)
 
 // Per-lane shading state ("cold": not needed while the lane walks) lives in HBM and is loaded /
 // stored only around the shading phase, so the walk phase's register footprint is the ray, the
@@ -1255,14 +1256,14 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                     atomicAdd(lhist + min(31 - __clz((int)steps), kHist - 1), 1u);
                     steps = 0;
                 }
-                if (!more) {
-                    // the winner's check against the reference BVH runs in the shading phase
-                    // (htri, ht) == (w.best_slot, w.best_t): the hit is already in place
-                    // (no winner: a miss -- or, for a bounded last-bounce walk, never expected: exact slow walk)
-                    state = (w.best_slot != kNone) ? ST_CHECK : (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
-                }
+                if (!more) state = ST_WALKED;
             }
         }
+        // the winner's check against the reference BVH runs in the shading phase
+        // (htri, ht) == (w.best_slot, w.best_t): the hit is already in place
+        // (no winner: a miss -- or, for a bounded last-bounce walk, never expected: exact slow walk)
+        if (state == ST_WALKED)
+            state = (w.best_slot != kNone) ? ST_CHECK : (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
 
         if (kCount) {
             const unsigned long long c = clock64();
