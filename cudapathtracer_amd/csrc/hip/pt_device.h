@@ -740,6 +740,8 @@ struct NoSetup {
     __device__ void operator()(W4&) const {}
 };
 // kTop: the caller guarantees S.ntop >= 1 (no per-step test of an empty LDS top).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wsometimes-uninitialized"   // (a lane's triangle words, read only if it has a leaf)
 template <bool kCount, bool kTop = false, class Setup = NoSetup>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
@@ -751,9 +753,16 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
     // (slots < 2^23, see kLeafBits: a full-rate 24-bit multiply; the slot is formed unconditionally
     // and selected, no branch)
-    const uint32_t tb = __umul24(leaf ? leaf4_slot(w) : 0u, (uint32_t)sizeof(DTri));
-    float4 A = glb_f4(tris, tb), B = glb_f4(reinterpret_cast<const char*>(tris) + 16, tb);
-    float e2z = *(__attribute__((address_space(1))) const float*)(reinterpret_cast<const char*>(tris) + 32 + tb);
+    // Only the lanes with a pending leaf load it (TA -3%, TD -1%, +0.8%; tools/gpu/pmc_ab.sh).  The
+    // other lanes' A, B, e2z are never read (pin_use below only orders the loads before the node's).
+    float4 A, B;
+    float e2z;
+    if (leaf) {
+        const uint32_t tb = __umul24(leaf4_slot(w), (uint32_t)sizeof(DTri));
+        A = glb_f4(tris, tb);
+        B = glb_f4(reinterpret_cast<const char*>(tris) + 16, tb);
+        e2z = *(__attribute__((address_space(1))) const float*)(reinterpret_cast<const char*>(tris) + 32 + tb);
+    }
     // a lane with no node to visit reads node 0 (the LDS copy when there is one)
     const uint32_t nidx = visit ? w.node : 0u;
     float4 NX, FX, NY, FY, NZ, FZ;
@@ -861,6 +870,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     }
     return w.node != kNone || leaf4_pending(w);
 }
+#pragma clang diagnostic pop
 
 // Exact walk for the rare rays the fast path does not take (outside the Markstein
 // preconditions, or a BVH4 winner the reference would not have tested): the culled near-first
