@@ -197,6 +197,22 @@ __device__ __forceinline__ void rng_init(Rng& s, uint64_t seed, uint32_t subseq,
     s.v0 = v0; s.v1 = v1; s.v2 = v2; s.v3 = v3; s.v4 = v4;
 }
 
+// v <- M v for a GF(2) matrix M in byte-sliced form (m: 20 x 256 entries of kJumpEntryWords words,
+// entry (j, x) = M * (x << 8j)): 20 independent lookups XORed together.
+__device__ __forceinline__ void jump_apply(uint32_t v[5], const uint32_t* __restrict__ m)
+{
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+#pragma unroll
+    for (int j = 0; j < 20; ++j) {
+        const uint32_t w = v[j >> 2];
+        const uint32_t x = (w >> (8 * (j & 3))) & 255u;
+        const uint32_t* e = m + ((size_t)j * 256 + x) * kJumpEntryWords;
+        const uint4 q = *reinterpret_cast<const uint4*>(e);
+        r0 ^= q.x; r1 ^= q.y; r2 ^= q.z; r3 ^= q.w; r4 ^= e[4];
+    }
+    v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+}
+
 // ------------------------------------------------------------------ geometry tests
 // triIntersect (modelLoader.h:49-83) on a precomputed {v0, e1, e2} record.
 __device__ __forceinline__ float tri_t(V3 o, V3 d, V3 v0, V3 e1, V3 e2)

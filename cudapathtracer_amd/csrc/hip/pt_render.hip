@@ -35,6 +35,10 @@ struct Args {
     const DMat* mats;
     const DLight* lights;
     const uint32_t* jump;
+    const uint32_t* jump_bytes;     // byte-position jump matrices J(b << 8) and J(b << 16), b < 256,
+                                    // byte-sliced (build_jump_byte_tables); null: per-bit jumps only
+    const uint32_t* seed_states;    // curand_init(seed, s0, 0) for s0 < 256: v0..v4 (kJumpEntryWords
+                                    // words each; seed_table), with jump_bytes
     float* out;
     unsigned long long* counters;   // [0] traced [1] reference [2] nodes [3] tris [4] samples
     uint32_t* tile_counter;
@@ -689,7 +693,25 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     }
     const uint32_t idx = morton2(px, py);
     Rng r;
-    rng_init(r, a.seed, idx, a.jump);
+    if (a.jump_bytes) {
+        // curand_init(seed, idx, 0) = J(idx) v(seed): the jump matrices are powers of one matrix,
+        // so they commute and J(idx) = J(idx & 0xff0000) J(idx & 0xff00) J(idx & 0xff) -- the low
+        // byte's product is tabulated per render (seed_states), the next two bytes' per context
+        // (jump_bytes): 40 lookups instead of 20 per set bit of idx
+        uint32_t v[5];
+        const uint32_t* p0 = a.seed_states + (size_t)(idx & 255u) * kJumpEntryWords;
+        for (int k = 0; k < 5; ++k) v[k] = p0[k];
+        const uint32_t b1 = (idx >> 8) & 255u, b2 = (idx >> 16) & 255u;
+        constexpr size_t kMat = (size_t)20 * 256 * kJumpEntryWords;
+        if (b1) jump_apply(v, a.jump_bytes + (size_t)b1 * kMat);
+        if (b2) jump_apply(v, a.jump_bytes + (size_t)(256u + b2) * kMat);
+        for (int k = 24; k < 32; ++k)   // (images beyond 4096 x 4096: the remaining bits one by one)
+            if ((idx >> k) & 1u) jump_apply(v, a.jump + (size_t)k * kMat);
+        r.d = rng_seed_d(a.seed);
+        r.v0 = v[0]; r.v1 = v[1]; r.v2 = v[2]; r.v3 = v[3]; r.v4 = v[4];
+    } else {
+        rng_init(r, a.seed, idx, a.jump);
+    }
     const bool lens = (idx == 0) || (a.cam.radius != 0.0f);
     V3 o, d = v3(0.0f, 0.0f, 0.0f);
     if (!lens) camera_ray(a.cam, px, py, false, 0.0f, 0.0f, &o, &d);   // the pixel's pinhole ray
@@ -712,6 +734,34 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
         st[(UW_CD + 1) * N + u] = __float_as_uint(d.y);
         st[(UW_CD + 2) * N + u] = __float_as_uint(d.z);
     }
+}
+
+// The per-render table of init_pixel_states: curand_init(seed, s0, 0) for the 256 low bytes s0.
+__global__ __launch_bounds__(256) void seed_table(Args a, uint32_t* __restrict__ out)
+{
+    Rng r;
+    rng_init(r, a.seed, threadIdx.x, a.jump);
+    uint32_t* e = out + (size_t)threadIdx.x * kJumpEntryWords;
+    e[0] = r.v0; e[1] = r.v1; e[2] = r.v2; e[3] = r.v3; e[4] = r.v4;
+}
+
+// Per context: the byte-sliced matrices J(b << 8) (m = b) and J(b << 16) (m = 256 + b), b < 256,
+// entry (j, x) = J * (x << 8j), each the product of the per-bit matrices J_k of b's set bits
+// (applied to the entry's basis combination through the per-bit byte-sliced tables).
+__global__ __launch_bounds__(256) void build_jump_byte_tables(const uint32_t* __restrict__ jb, uint32_t* __restrict__ out)
+{
+    const uint32_t g = blockIdx.x * 256u + threadIdx.x;   // (m, j, x), x fastest
+    if (g >= 512u * 20u * 256u) return;
+    const uint32_t x = g & 255u, j = (g >> 8) % 20u, m = (g >> 8) / 20u;
+    const uint32_t b = m & 255u, shift = (m < 256u) ? 8u : 16u;
+    uint32_t v[5] = {0u, 0u, 0u, 0u, 0u};
+    v[j >> 2] = x << (8 * (j & 3));
+    constexpr size_t kMat = (size_t)20 * 256 * kJumpEntryWords;
+    for (uint32_t i = 0; i < 8; ++i)
+        if ((b >> i) & 1u) jump_apply(v, jb + (size_t)(shift + i) * kMat);
+    uint32_t* e = out + (size_t)g * kJumpEntryWords;
+    e[0] = v[0]; e[1] = v[1]; e[2] = v[2]; e[3] = v[3]; e[4] = v[4];
+    e[5] = 0u; e[6] = 0u; e[7] = 0u;
 }
 
 // Split slots: the running mean of kernel.cu:551-552, in sample order, over the stored
@@ -1499,6 +1549,9 @@ struct pt_ctx {
     DMat* mats = nullptr;
     DLight* lights = nullptr;
     uint32_t* jump = nullptr;
+    uint32_t* jump_bytes = nullptr;   // byte-position jump matrices (built on the first wavefront render)
+    uint32_t* seed_states = nullptr;  // per-render seed_table output
+    bool use_jump_bytes = true;       // PT_JUMP_BYTES=0: per-bit jumps only
     unsigned long long* counters = nullptr;
     uint32_t* tile_counter = nullptr;
     float* scratch_out = nullptr;
@@ -1728,6 +1781,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         while ((1u << bits) < nn) ++bits;
         c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_JUMP_BYTES")) c->use_jump_bytes = atoi(e) != 0;
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
             const int v = atoi(e);
             c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
@@ -1957,7 +2011,7 @@ void pt_destroy(pt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
-                    c->lights, c->jump, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
+                    c->lights, c->jump, c->jump_bytes, c->seed_states, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
@@ -2203,6 +2257,17 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_times), times.size() * 8));
             HIP_TRY(hipMemsetAsync(d_times, 0, times.size() * 8, stream));
             b.lane_times = d_times;
+        }
+        if (c->use_jump_bytes) {
+            if (!c->jump_bytes) {   // once per context: 512 byte-sliced 160x160 GF(2) matrices (84 MB)
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->jump_bytes), (size_t)512 * 20 * 256 * kJumpEntryWords * 4));
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->seed_states), (size_t)256 * kJumpEntryWords * 4));
+                hipLaunchKernelGGL(build_jump_byte_tables, dim3(512 * 20), dim3(256), 0, stream, c->jump, c->jump_bytes);
+                HIP_TRY(hipGetLastError());
+            }
+            hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, c->seed_states);
+            b.jump_bytes = c->jump_bytes;
+            b.seed_states = c->seed_states;
         }
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
         if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
