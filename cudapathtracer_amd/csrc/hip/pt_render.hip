@@ -775,12 +775,34 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     const size_t pix = (size_t)py * (size_t)a.w + px;
     const double* L = a.lbuf + (size_t)t * a.spp * 3;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-    for (int n = 1; n <= a.spp; ++n, L += 3) {
+    // one sample: the six quotients by fn as one IEEE reciprocal + Markstein corrections (RN(x/fn)
+    // for finite x clear of under/overflow, as in the render kernel's sample end) -- else the wave
+    // divides
+    auto step = [&](int n, double l0, double l1, double l2) {
         const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
-        m0 = (m0 * fn1) / fn + L[0] / fn;
-        m1 = (m1 * fn1) / fn + L[1] / fn;
-        m2 = (m2 * fn1) / fn + L[2] / fn;
+        const double x0 = m0 * fn1, x1 = m1 * fn1, x2 = m2 * fn1;
+        if (__ballot(!(quot_ok(x0) && quot_ok(x1) && quot_ok(x2) && quot_ok(l0) && quot_ok(l1) && quot_ok(l2))) == 0ull) {
+            const double rf = 1.0 / fn;
+            m0 = div_mk_d(x0, fn, rf) + div_mk_d(l0, fn, rf);
+            m1 = div_mk_d(x1, fn, rf) + div_mk_d(l1, fn, rf);
+            m2 = div_mk_d(x2, fn, rf) + div_mk_d(l2, fn, rf);
+        } else {
+            m0 = x0 / fn + l0 / fn;
+            m1 = x1 / fn + l1 / fn;
+            m2 = x2 / fn + l2 / fn;
+        }
+    };
+    // eight samples' loads issued together (the lane's samples are contiguous: one dependent round
+    // trip per eight samples instead of per sample)
+    int n = 1;
+    for (; n + 7 <= a.spp; n += 8, L += 24) {
+        double v[24];
+#pragma unroll
+        for (int k = 0; k < 24; ++k) v[k] = L[k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) step(n + k, v[3 * k], v[3 * k + 1], v[3 * k + 2]);
     }
+    for (; n <= a.spp; ++n, L += 3) step(n, L[0], L[1], L[2]);
     float* o3 = a.out + pix * 3;
     o3[0] = (float)m0;
     o3[1] = (float)m1;

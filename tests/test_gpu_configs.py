@@ -139,3 +139,19 @@ def test_lds_top_nodes_bit_identical(standin, monkeypatch, top):
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
     if top == "0":
         _check(s, img, cam_kw, w, h, spp, 3, _spread(w, h, 32, 5))
+
+
+@pytest.mark.parametrize("jump_bytes", ["1", "0"])
+def test_wide_image_seeding_beyond_24_morton_bits(monkeypatch, jump_bytes):
+    """curand_init of a pixel whose Morton index has bits >= 24 (x >= 4096): the byte-position jump
+    tables cover bits 0..23, the rest are applied bit by bit (init_pixel_states); both seeding
+    forms (PT_JUMP_BYTES) equal the oracle's curand_init bit for bit there and elsewhere."""
+    monkeypatch.setenv("PT_JUMP_BYTES", jump_bytes)
+    s = load_scene("cornell")
+    w, h, spp = 4104, 2, 2
+    cam_kw = scenes.CORNELL_CAMERA
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(pt.make_camera(width=w, height=h, **cam_kw), w, h, spp, bounces=3)
+    assert st["samples"] == w * h * spp
+    pix = np.array([0, 1, 255, 256, 4095, 4096, 4097, 4103, w + 4096, w + 4103, w * h - 1], dtype=np.uint32)
+    _check(s, img, cam_kw, w, h, spp, 3, pix)
