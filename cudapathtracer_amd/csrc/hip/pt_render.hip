@@ -60,6 +60,8 @@ struct Args {
     uint32_t wf_iters;              // shading iterations a lane may run per pass before yielding
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
     uint32_t top_nodes;             // wavefront kernel: BVH4 nodes 0..top_nodes-1 staged in LDS
+    uint32_t tile_fast4;            // tile kernel: trace with the render-path BVH4 walk (winner check, exact
+                                    // slow walk as fallback) instead of the reference-BVH culled walk
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
@@ -153,15 +155,50 @@ struct Tracer {
     uint32_t ko[3], kd[3];
     Hit kh;
 
-    __device__ Hit trace(V3 o, V3 d)
+
+    __device__ __forceinline__ Hit trace(V3 o, V3 d)
     {
         ++traced;
         Hit h;
         h.tri = -1;
         h.t = kMaxFloat;
         if (a->num_tris > 0) {
-            if (kRefWalk) h = trace_reference<kCount>(o, d, a->rnodes, a->tris_orig, stack, lane, cnt);
-            else h = trace_culled<kCount>(o, d, a->root, a->nodes, a->tris_leaf, stack, lane, a->cull_rel, a->cull_abs, cnt);
+            if (kRefWalk) {
+                h = trace_reference<kCount>(o, d, a->rnodes, a->tris_orig, stack, lane, cnt);
+            } else if (a->tile_fast4) {
+                // the wavefront kernel's walk, run to its end by this lane (DESIGN.md "Traversal"); its
+                // LDS rings (this block's one wave) and HBM spill column
+                const uint32_t lane_off = (blockIdx.x * 64u + (uint32_t)lane) * 4u;
+                Stack4 S;
+                S.ring = stack + lane;
+                S.stride = a->spill_stride;
+                S.spill_base = a->spill;
+                S.lane_off = &lane_off;
+                S.off_mask = ~0u;
+                if ((a->scene_fast != 0u) && ray_fast(o, d)) {
+                W4 w;
+                if (walk4_begin(w, o, d, a->acc_root, a->cull_abs)) {
+                    while (walk4_step<kCount>(w, o, d, a->nodes4, a->acc_tris, S, a->cull_rel, a->cull_abs, a->node_mask,
+                                              cnt)) {
+                    }
+                    h.t = w.best_t;
+                    bool ok = true;
+                    if (w.best_slot != kNone) {
+                        const float4 C = a->acc_tris[w.best_slot].c;
+                        h.tri = (int32_t)__float_as_uint(C.y);
+                        ok = ref_tested(__float_as_uint(C.w), o, d, a->rnodes, a->rparent);
+                    }
+                    if (!ok)
+                        trace_slow(o, d, a->root, a->nodes, a->tris_leaf, S.spill(), S.stride, a->cull_rel, a->cull_abs,
+                                   &h.tri, &h.t, cnt.tri_counts);
+                }
+                } else {   // outside the Markstein preconditions: the exact slow walk
+                    trace_slow(o, d, a->root, a->nodes, a->tris_leaf, S.spill(), S.stride, a->cull_rel, a->cull_abs,
+                               &h.tri, &h.t, cnt.tri_counts);
+                }
+            } else {
+                h = trace_culled<kCount>(o, d, a->root, a->nodes, a->tris_leaf, stack, lane, a->cull_rel, a->cull_abs, cnt);
+            }
         }
         if (a->num_spheres) apply_spheres(*a, o, d, &h.tri, &h.t);
         return h;
@@ -436,10 +473,14 @@ __device__ __forceinline__ T fresh(T x)
     return x;
 }
 
+// (kFresh: the image size made opaque at its use -- the wavefront kernel's register discipline; the
+// tile kernel, whose arguments may live in memory, takes them as they are)
+template <bool kFresh = true>
 __device__ __forceinline__ void camera_ray(const Cam& cam, uint32_t px, uint32_t py, bool lens, float u1, float u2,
                                            V3* o, V3* d)
 {
-    V3 film = v3((float)px / (float)fresh(cam.w) - 0.5f, (float)py / (float)fresh(cam.h) - 0.5f, 0.0f);
+    const int cw = kFresh ? fresh(cam.w) : cam.w, ch = kFresh ? fresh(cam.h) : cam.h;
+    V3 film = v3((float)px / (float)cw - 0.5f, (float)py / (float)ch - 0.5f, 0.0f);
     V3 lo = v3(0.0f, 0.0f, 0.0f);
     if (lens) {
         const float r = cam.radius * sqrtf(u1);
@@ -509,7 +550,7 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
             float u1 = 0.0f, u2 = 0.0f;
             if (lens) { u1 = rng_uniform(rng); u2 = rng_uniform(rng); }
             V3 o, d;
-            camera_ray(a.cam, px, py, lens, u1, u2, &o, &d);
+            camera_ray<false>(a.cam, px, py, lens, u1, u2, &o, &d);
             C3 L;
             if (kIntegrator == PT_INTEGRATOR_HEAD) L = radiance_head(a, tr, o, d, rng, memo);
             else L = radiance_unidir(a, tr, o, d, rng, skip_dead, memo);
@@ -1574,6 +1615,7 @@ struct pt_ctx {
     uint32_t* jump_bytes = nullptr;   // byte-position jump matrices (built on the first wavefront render)
     uint32_t* seed_states = nullptr;  // per-render seed_table output
     bool use_jump_bytes = true;       // PT_JUMP_BYTES=0: per-bit jumps only
+    bool tile_fast4 = true;           // PT_TILE_FAST4=0: the tile kernel walks the reference BVH (culled)
     unsigned long long* counters = nullptr;
     uint32_t* tile_counter = nullptr;
     float* scratch_out = nullptr;
@@ -1804,6 +1846,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_JUMP_BYTES")) c->use_jump_bytes = atoi(e) != 0;
+        if (const char* e = getenv("PT_TILE_FAST4")) c->tile_fast4 = atoi(e) != 0;
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
             const int v = atoi(e);
             c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
@@ -2112,7 +2155,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const bool refwalk = (p->flags & PT_FLAG_REFERENCE_TRAVERSAL) != 0;
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
     const uint32_t levels = (uint32_t)c->depth + 2;
-    a.stack_words = levels * 128;
+    a.stack_words = std::max<uint32_t>(levels * 128, (uint32_t)kWaveLdsWords);   // (culled walk's stack, or the BVH4 rings)
     const size_t lds = (size_t)a.stack_words * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
 
@@ -2143,6 +2186,9 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const uint32_t waves_per_cu = 16;
     uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
     if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
+    // the tile kernel traces with the render-path BVH4 walk under the wavefront kernel's conditions
+    // (PT_TILE_FAST4=0: the reference-BVH culled walk, as before)
+    a.tile_fast4 = (!refwalk && !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam && c->tile_fast4 && c->num_tris > 0) ? 1u : 0u;
     HIP_TRY(hipEventRecord(c->ev0, stream));
     if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
         // 4 waves per block; per wave an LDS ring of kRing packed entries x 64 lanes, deeper
@@ -2307,6 +2353,11 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             write_lane_timing(timing_path, times, (size_t)blocks * 256, p->shard_count);
         }
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
+        if (a.tile_fast4) {   // the BVH4 walk's ring overflow and the slow walk's stack: one HBM column per lane
+            if (int rc = ensure_spill(c, stack_words_per_lane(c) * (size_t)grid * 64)) return rc;
+            a.spill = c->spill;
+            a.spill_stride = grid * 64;
+        }
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
         if (p->integrator == PT_INTEGRATOR_HEAD) {
             if (refwalk) { if (count) PT_LAUNCH(1, true, true); else PT_LAUNCH(1, true, false); }

@@ -155,3 +155,30 @@ def test_wide_image_seeding_beyond_24_morton_bits(monkeypatch, jump_bytes):
     assert st["samples"] == w * h * spp
     pix = np.array([0, 1, 255, 256, 4095, 4096, 4097, 4103, w + 4096, w + 4103, w * h - 1], dtype=np.uint32)
     _check(s, img, cam_kw, w, h, spp, 3, pix)
+
+
+@pytest.mark.parametrize("fast4", ["1", "0"])
+def test_head_integrator_tile_walks_bit_identical(standin, monkeypatch, fast4):
+    """Integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the 262K stand-in: the tile
+    kernel tracing with the render-path BVH4 walk (default; winner check + exact slow walk) and
+    with the reference-BVH culled walk (PT_TILE_FAST4=0) render the same bits as the
+    reference-order walk, and a spread of pixels equals the oracle."""
+    s, r = standin
+    w, h, spp = 160, 96, 4
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    cam = pt.make_camera(width=w, height=h, **cam_kw)
+    ref, _ = r.render(cam, w, h, spp, bounces=3, integrator=1, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
+    monkeypatch.setenv("PT_TILE_FAST4", fast4)
+    with pt.Renderer(s, 0) as r2:
+        img, st = r2.render(cam, w, h, spp, bounces=3, integrator=1)
+    assert st["samples"] == w * h * spp
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    if fast4 == "1":
+        import oracle
+        osc = oracle.OracleScene(s.arrays())
+        ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"], w, h)
+        pix = _spread(w, h, 24, 6)
+        o, _ = oracle.render(osc, ocam, w, h, spp, 3, 1, 1234, pixels=pix)
+        a = img.reshape(-1, 3)[pix]
+        b = o.reshape(-1, 3)[pix].astype(np.float32)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
