@@ -911,6 +911,9 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
     const Args& a = kernel_args_opaque();
     const int D = a.bounces;
     SEC(SEC_PASS);
+    // the words every pass needs: four 16-B cells (issued first: their round trip overlaps the
+    // winner check's two dependent ones)
+    const uint4 k0 = R.ld4(CW_N), k1 = R.ld4(CW_RNG_V0), k2 = R.ld4(CW_WGT), k3 = R.ld4(CW_WGT + 4);
     if (state == ST_CHECK) {
         SEC(SEC_CHECK);
         // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
@@ -919,8 +922,6 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
         htri = (int32_t)__float_as_uint(C.y);
         state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
     }
-    // the words every pass needs: four 16-B cells
-    const uint4 k0 = R.ld4(CW_N), k1 = R.ld4(CW_RNG_V0), k2 = R.ld4(CW_WGT), k3 = R.ld4(CW_WGT + 4);
     int n = (int)k0.x, i = (int)k0.y;
     uint32_t fl = k0.z;
     Rng rng;
