@@ -89,6 +89,10 @@ struct Args {
     uint32_t num_tris;
     uint32_t sphere_mat_base;       // material of sphere i = mats[sphere_mat_base + i]
     uint32_t* tri_counts;           // PT_FLAG_COUNT: per-triangle test counts by original id (kernel.cu:133)
+    const float4* shade_m;          // per triangle 48 B: {normal, Le.r}, {albedo, Le.g}, {Le.b, material, -, -} --
+                                    // the material's f64 colours as floats, set only when every material's colours
+                                    // are float-exact (MTL values are floats): one fetch per bounce, not two
+                                    // dependent ones (shade, then mats); null: shade + mats
     const DTri* emis;               // last-bounce light probe: the emissive triangles' records (see begin_trace)
     uint32_t num_emis;              // 0 = probe off
     unsigned long long* lane_times; // diagnostic (PT_LANE_TIMING): wall clock of each lane's end, then each
@@ -1034,9 +1038,21 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
             if ((double)t < 0.001) wgt = c3(0, 0, 0);
             if (t > kMaxFloat - 1) { wgt = c3(0, 0, 0); tri = 0; t = 0; }
             const V3 pos = ro + rd * t;
-            const DMat* cm = a.mats + prim_mat(a, tri);
-            const V3 normal = prim_normal(a, tri, pos);
-            if (cm->emission[0] != 0) {
+            V3 normal;
+            C3 m_em, m_alb;   // the material's emission and albedo (materialDesc, f64)
+            if (a.shade_m && (uint32_t)tri < a.num_tris) {
+                const float4* rec = a.shade_m + 3 * (size_t)(uint32_t)tri;
+                const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+                normal = v3(q0.x, q0.y, q0.z);
+                m_em = c3(q0.w, q1.w, q2.x);
+                m_alb = c3(q1.x, q1.y, q1.z);
+            } else {
+                const DMat* cm = a.mats + prim_mat(a, tri);
+                normal = prim_normal(a, tri, pos);
+                m_em = mat_emission(cm);
+                m_alb = mat_albedo(cm);
+            }
+            if (m_em.r != 0) {
                 SEC(SEC_EMIT);
                 C3 acc = c3(0.0, 0.0, 0.0);
                 if (!(fl & CF_ACC0)) {
@@ -1045,7 +1061,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     acc = c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2.x, a2.y));
                 }
                 fl &= ~CF_ACC0;
-                acc = cadd(acc, cmul(wgt, mat_emission(cm)));
+                acc = cadd(acc, cmul(wgt, m_em));
                 R.st4(CW_ACC, dlo(acc.r), dhi(acc.r), dlo(acc.g), dhi(acc.g)); R.st2(CW_ACC + 4, dlo(acc.b), dhi(acc.b));
                 wgt = c3(0, 0, 0);
             }
@@ -1114,7 +1130,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                 f = cos_l * cos_o / dot(vec, vec);   // G
                 i = (i > D - 2) ? i : D - 2;
             }
-            C3 bw = cmulf(brdf(cm), f);
+            C3 bw = cmulf(cmulf(m_alb, (float)(1 / 3.14159)), f);   // brdf (kernel.cu:101-104) * f
             if (!cosb) bw = cmulf(bw, fresh(a.total_light_area));
             wgt = cmul(wgt, bw);
             ro = pos;
@@ -1613,6 +1629,7 @@ struct pt_ctx {
     DMat* mats = nullptr;
     DLight* lights = nullptr;
     uint32_t* jump = nullptr;
+    float4* shade_m = nullptr;        // merged shading records (Args::shade_m), or none
     uint32_t* jump_bytes = nullptr;   // byte-position jump matrices (built on the first wavefront render)
     uint32_t* seed_states = nullptr;  // per-render seed_table output
     bool use_jump_bytes = true;       // PT_JUMP_BYTES=0: per-bit jumps only
@@ -1989,6 +2006,26 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         sh[i].nx = sc->tris[i].norm.x; sh[i].ny = sc->tris[i].norm.y; sh[i].nz = sc->tris[i].norm.z;
         sh[i].mat = sc->tris[i].mat;
     }
+    // the merged per-triangle shading record (Args::shade_m) when every material colour is a float
+    std::vector<float4> shm;
+    {
+        bool exact = nt > 0 && !getenv("PT_NO_SHADE_M");
+        for (uint32_t i = 0; i < sc->num_mats && exact; ++i)
+            for (int q = 0; q < 3; ++q)
+                exact = exact && (double)(float)sc->mats[i].albedo[q] == sc->mats[i].albedo[q] &&
+                        (double)(float)sc->mats[i].emission[q] == sc->mats[i].emission[q];
+        if (exact) {
+            shm.resize((size_t)3 * nt);
+            for (uint32_t i = 0; i < nt; ++i) {
+                const pt_material& m = sc->mats[sc->tris[i].mat];
+                shm[3 * (size_t)i] = make_float4(sc->tris[i].norm.x, sc->tris[i].norm.y, sc->tris[i].norm.z, (float)m.emission[0]);
+                shm[3 * (size_t)i + 1] = make_float4((float)m.albedo[0], (float)m.albedo[1], (float)m.albedo[2], (float)m.emission[1]);
+                float mbits;
+                memcpy(&mbits, &sc->tris[i].mat, 4);
+                shm[3 * (size_t)i + 2] = make_float4((float)m.emission[2], mbits, 0.0f, 0.0f);
+            }
+        }
+    }
     // scene materials, then one per sphere (sphere.h diffuse / emm)
     std::vector<DMat> mt(sc->num_mats + sc->num_spheres);
     for (uint32_t i = 0; i < sc->num_mats; ++i) {
@@ -2052,7 +2089,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     int rc = PT_OK;
     lap("records + jump/tone tables");
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
-        (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (rc = upload(&c->mats, mt)) ||
+        (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (!shm.empty() && (rc = upload(&c->shade_m, shm))) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
         (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) ||
         (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u))) ||
@@ -2077,7 +2114,7 @@ void pt_destroy(pt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
-                    c->lights, c->jump, c->jump_bytes, c->seed_states, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
+                    c->lights, c->jump, c->jump_bytes, c->seed_states, c->shade_m, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
                     c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
@@ -2135,7 +2172,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     Args a;
     memset(&a, 0, sizeof(a));
     a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
-    a.shade = c->shade; a.mats = c->mats; a.lights = c->lights; a.jump = c->jump;
+    a.shade = c->shade; a.mats = c->mats; a.lights = c->lights; a.jump = c->jump; a.shade_m = c->shade_m;
     a.out = d_out; a.counters = c->counters; a.tile_counter = c->tile_counter;
     a.num_lights = c->num_lights; a.total_light_area = c->total_light_area;
     a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;

@@ -182,3 +182,17 @@ def test_head_integrator_tile_walks_bit_identical(standin, monkeypatch, fast4):
         a = img.reshape(-1, 3)[pix]
         b = o.reshape(-1, 3)[pix].astype(np.float32)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_merged_shading_records_bit_identical(standin, monkeypatch):
+    """The wavefront bounce reads a triangle's normal and its material's colours from one merged
+    48-B record (Args::shade_m, used when every material colour is a float); PT_NO_SHADE_M=1 reads
+    the shading record and then the material (two dependent fetches): the same bits."""
+    s, r = standin
+    w, h, spp = 320, 180, 8
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    a, _ = r.render(cam, w, h, spp, bounces=5)
+    monkeypatch.setenv("PT_NO_SHADE_M", "1")
+    with pt.Renderer(s, 0) as r2:
+        b, _ = r2.render(cam, w, h, spp, bounces=5)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
