@@ -951,7 +951,10 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
         return false;
     };
     // start sample n of pixel (px, py): camera ray, then memo or trace
-    auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
+    // (c7 / c8: the record's cells 7 (pixel, memo) and 8 (pinhole direction) when the caller already
+    // holds them -- fetched with the previous sample's end, or just written by the refill -- so the
+    // start costs no dependent fetch)
+    auto start_sample = [&](uint32_t px, uint32_t py, bool have_cells, uint4 c7, uint4 c8) -> bool {
         i = 0;
         fl |= CF_ACC0;   // acc = 0 (stored on the sample's first emission)
         wgt = c3(1, 1, 1);
@@ -968,20 +971,20 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
             }
         } else {
             ro = v3(0.0f, 0.0f, 0.0f) + v3(fresh(a.cam.pos[0]), fresh(a.cam.pos[1]), fresh(a.cam.pos[2]));   // as camera_ray forms it
-            const uint4 cd = R.ld4(CW_CD);
+            const uint4 cd = have_cells ? c8 : R.ld4(CW_CD);
             rd = v3(__uint_as_float(cd.x), __uint_as_float(cd.y), __uint_as_float(cd.z));
         }
         wave_count(lcnt + 1, lane);
         if (fl & CF_HAVE) {
             SEC(SEC_MEMO);
-            const uint2 mm = R.ld2(CW_MTRI);
+            const uint2 mm = have_cells ? make_uint2(c7.z, c7.w) : R.ld2(CW_MTRI);
             htri = (int32_t)mm.x; ht = __uint_as_float(mm.y);
             fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
             return true;
         }
         if (fl & CF_SHARE) {
             // the pixel's chunk 0 may have published the (sample-invariant) primary hit
-            const uint32_t q = R.ld(CW_Q);
+            const uint32_t q = have_cells ? c8.w : R.ld(CW_Q);
             // hit and flag in one word: a relaxed agent-scope load (coherent across the XCDs' L2s
             // for this word) needs no acquire, i.e. no invalidation of this XCD's L2
             const uint64_t mv = __hip_atomic_load(reinterpret_cast<uint64_t*>(a.pmemo) + q, __ATOMIC_RELAXED,
@@ -1142,8 +1145,10 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
             if (i >= D) {
                 wave_count(lcnt + 2, lane);
                 SEC(SEC_SAMPLE_END);
-                const uint2 pxy = R.ld2(CW_PX);
-                const uint32_t px = pxy.x, py = pxy.y;
+                // cells 7 (pixel, memo) and 8 (pinhole direction) with the accumulator and mean: the
+                // next sample's start needs no fetch of its own
+                const uint4 c7 = R.ld4(CW_PX), c8 = R.ld4(CW_CD);
+                const uint32_t px = c7.x, py = c7.y;
                 // acc and the running mean: cells 4..6 = acc.r, acc.g | acc.b, m0 | m1, m2
                 uint4 a01 = make_uint4(0u, 0u, 0u, 0u);
                 if (!(fl & CF_ACC0)) a01 = R.ld4(CW_ACC);
@@ -1190,7 +1195,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     }
                 }
                 ++n;
-                again = start_sample(px, py);
+                again = start_sample(px, py, true, c7, c8);
                 break;
             }
             // Last-bounce light probe.  The hit of bounce D-1 only decides the emission it adds
@@ -1276,16 +1281,21 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     n = (int)(n0 & 0x7fffffffu);
                     const bool split = u >= a.nwhole;
                     fl = (n0 >> 31) ? CF_LENS : CF_CAMC;
-                    if (!(fl & CF_LENS))
-                        R.st4(CW_CD, a.pix_states[UW_CD * N + u], a.pix_states[(UW_CD + 1) * N + u],
-                              a.pix_states[(UW_CD + 2) * N + u], a.pix_states[UW_TQ * N + u]);
+                    uint4 c8 = make_uint4(0u, 0u, 0u, 0u);
+                    if (!(fl & CF_LENS)) {
+                        c8 = make_uint4(a.pix_states[UW_CD * N + u], a.pix_states[(UW_CD + 1) * N + u],
+                                        a.pix_states[(UW_CD + 2) * N + u], a.pix_states[UW_TQ * N + u]);
+                        R.st4(CW_CD, c8.x, c8.y, c8.z, c8.w);
+                    }
                     if (split) fl |= CF_SPLIT;
                     if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
                         fl |= (n == 1) ? CF_OWNER : CF_SHARE;   // (chunk 0 starts at sample 1)
                     R.st2(CW_PX, px, py);
                     if (split && (fl & CF_LENS)) R.st(CW_Q, a.pix_states[UW_TQ * N + u]);
                     R.st2(CW_M, 0u, 0u); R.st4(CW_M + 2, 0u, 0u, 0u, 0u);
-                    again = start_sample(px, py);
+                    // (a new unit: no memo yet; its pinhole direction and slot are in c8 -- a lens
+                    // unit reads neither, and its slot from the record)
+                    again = start_sample(px, py, !(fl & CF_LENS), make_uint4(0u, 0u, 0u, 0u), c8);
                 }
             }
         }
