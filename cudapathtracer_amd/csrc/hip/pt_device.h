@@ -540,6 +540,19 @@ __device__ __forceinline__ bool ref_tested(uint32_t parent, V3 o, V3 d,
     }
 }
 
+// The same with the reference parent's record already fetched (a, b: its first two 16-B words; a
+// per-slot copy, so it arrives with the winner's ids instead of behind them).
+__device__ __forceinline__ bool ref_tested_box(float4 a, float4 b, uint32_t parent, V3 o, V3 d,
+                                               const RNode* __restrict__ rnodes, const uint32_t* __restrict__ rparent)
+{
+    const bool zero_dir = d.x == 0.0f || d.y == 0.0f || d.z == 0.0f;
+    const V3 y = v3(rcp_or_inf(d.x), rcp_or_inf(d.y), rcp_or_inf(d.z));
+    float ti, to;
+    if (!slab<true>(o, d, y, a.x, a.y, a.z, a.w, b.x, b.y, &ti, &to)) return false;
+    if (!zero_dir || parent == 0u) return true;
+    return ref_tested(rparent[parent], o, d, rnodes, rparent);
+}
+
 // leaf queue entry: (the node's first leaf slot << kLeafBits) | mask of the entered leaves' slots
 // (a node's leaf children hold at most kLeafBits triangles; slots < 2^(31 - kLeafBits))
 constexpr uint32_t kLeafBits = 8;

@@ -65,6 +65,9 @@ struct Args {
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
+    const RNode* wbox;              // per render-path slot: its triangle's reference parent node (left/right
+                                    // replaced by the parent's index) -- the winner check's box, fetched
+                                    // with the slot's ids
     uint32_t* spill;                // LDS-stack overflow, entry k of lane g at spill[(k-kRing)*stride + g]
     uint32_t spill_stride;
     uint32_t cold_stride;           // records of the cold array (one per resident lane)
@@ -923,8 +926,9 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
         // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
         // (rare), the exact reference-BVH walk redoes the ray
         const float4 C = a.acc_tris[htri].c;
+        const float4 b0 = reinterpret_cast<const float4*>(a.wbox + htri)[0], b1 = reinterpret_cast<const float4*>(a.wbox + htri)[1];
         htri = (int32_t)__float_as_uint(C.y);
-        state = ref_tested(__float_as_uint(C.w), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
+        state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
     }
     int n = (int)k0.x, i = (int)k0.y;
     uint32_t fl = k0.z;
@@ -1679,6 +1683,7 @@ struct pt_ctx {
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
+    RNode* wbox = nullptr;
     uint32_t* spill = nullptr;
     size_t spill_words = 0;
     uint32_t* pix_states = nullptr;   // init_pixel_states output (kUnitWords per work unit)
@@ -1997,6 +2002,15 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (!(sc->bvh[i].left & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].left] = i;
         if (!(sc->bvh[i].right & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].right] = i;
     }
+    // per render-path slot: the reference parent's node of its triangle (Args::wbox)
+    std::vector<RNode> wb(std::max<size_t>(at.size(), 1));
+    for (size_t sl = 0; sl < at.size(); ++sl) {
+        uint32_t parent;
+        memcpy(&parent, &at[sl].c.w, 4);
+        wb[sl] = rn[parent];
+        wb[sl].left = parent;
+        wb[sl].right = 0u;
+    }
     // last-bounce light probe (shade_lane begin_trace): every triangle whose material has
     // emission.r != 0 (the integrator's emission test, kernel.cu:453 -- not the caller's light list)
     std::vector<DTri> em;
@@ -2101,7 +2115,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (!shm.empty() && (rc = upload(&c->shade_m, shm))) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
-        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) ||
+        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) || (rc = upload(&c->wbox, wb)) ||
         (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u))) ||
         (rc = upload(&c->emis, em))) {
         pt_destroy(c);
@@ -2125,7 +2139,7 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->jump_bytes, c->seed_states, c->shade_m, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->nodes4, c->acc_tris, c->rparent, c->spill, c->pix_states, c->lbuf, c->pmemo,
+                    c->nodes4, c->acc_tris, c->rparent, c->wbox, c->spill, c->pix_states, c->lbuf, c->pmemo,
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -2216,6 +2230,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.nodes4 = c->nodes4;
     a.acc_tris = c->acc_tris;
     a.rparent = c->rparent;
+    a.wbox = c->wbox;
     memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
     // the render-path BVH's box margin assumes ray origins within ~2^6 of the scene extent
     const float cam_ext = std::fmax(std::fabs(cam->pos.x), std::fmax(std::fabs(cam->pos.y), std::fabs(cam->pos.z)));
