@@ -733,8 +733,8 @@ constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
 constexpr uint32_t kTopNodeBytes = 112;
 // what fits next to the rings with 5 blocks of 256 threads per CU: LDS is granted in 1280-B granules,
 // 32000 B per block = 4 x 5120 B of rings + 160 B of counters + 208 B of light-probe emitters
-// (pt_render.hip) + 99 x 112 B
-constexpr uint32_t kTopNodesMax = 99;
+// (pt_render.hip) + 240 B of NEE light records + 97 x 112 B
+constexpr uint32_t kTopNodesMax = 97;
 
 template <bool kCount>
 __device__ __forceinline__ void push4(W4& w, const Stack4& S, uint32_t e, Counters& cnt)

@@ -678,7 +678,10 @@ constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the ima
 constexpr uint32_t kMaxProbeEmitters = 4;    // last-bounce light probe: at most this many emissive triangles
 // LDS of a wavefront block after the counters: the probe's emitter count (16 B) and records, then the
 // staged BVH4 top nodes
-constexpr uint32_t kProbeLdsBytes = 16 + kMaxProbeEmitters * (uint32_t)sizeof(DTri);
+// then the NEE light records (lights[0..num_lights], the last being "nothing picked") when at most
+// kLdsLights of them: the area-CDF pick and the picked record read LDS, not two dependent fetches
+constexpr uint32_t kLdsLights = 5;
+constexpr uint32_t kProbeLdsBytes = 16 + kMaxProbeEmitters * (uint32_t)sizeof(DTri) + kLdsLights * (uint32_t)sizeof(DLight);
 __device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c, uint32_t chunks)
 {
     return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / chunks);
@@ -1092,12 +1095,16 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                 // area-CDF pick (pick_light); the scan stops once randArea <= 0
                 float ra = a.total_light_area * r1;
                 uint32_t sel = a.num_lights;
+                // (the records staged in the block's LDS when few; the pick reads them there)
+                const DLight* const lt = (a.num_lights < kLdsLights)
+                                             ? reinterpret_cast<const DLight*>(lprobe + 4 + kMaxProbeEmitters * 12)
+                                             : a.lights;
                 for (uint32_t j = 0; j < a.num_lights && ra > 0; ++j) {
-                    const float area = a.lights[j].area;
+                    const float area = lt[j].area;
                     if (ra < area && ra > 0) sel = j;
                     ra -= area;
                 }
-                L = a.lights + sel;
+                L = lt + sel;
                 if (L->pad != 0.0f) { need_sc = true; ang = r3; }   // sphere light: phi = 2*3.14159*v
             } else {
                 SEC(SEC_COSINE);
@@ -1357,6 +1364,9 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     // the light probe's emitters (count, then records), then the top of the BVH4 (kTopNodeBytes per node)
     uint32_t* const lprobe = reinterpret_cast<uint32_t*>(lcnt + 4 + (kSections + kHist) / 2);
     if (threadIdx.x == 0) lprobe[0] = a.num_emis;
+    if (a.num_lights < kLdsLights)
+        for (uint32_t k = threadIdx.x; k < (a.num_lights + 1) * 3; k += blockDim.x)
+            reinterpret_cast<float4*>(lprobe + 4 + kMaxProbeEmitters * 12)[k] = reinterpret_cast<const float4*>(a.lights)[k];
     for (uint32_t k = threadIdx.x; k < a.num_emis * 3; k += blockDim.x)
         reinterpret_cast<float4*>(lprobe + 4)[k] = reinterpret_cast<const float4*>(a.emis)[k];
     float4* const ltop = reinterpret_cast<float4*>(reinterpret_cast<char*>(lprobe) + kProbeLdsBytes);
