@@ -1678,7 +1678,8 @@ struct pt_ctx {
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
     int wf_tail_chunks = 6;         // chunks of each tail pixel (PT_WF_TAIL_CHUNKS; 1 = no tail split)
-    double wf_tail_px = 0.75;       // tail pixels per resident lane (PT_WF_TAIL_PX)
+    double wf_tail_px = 1.5;        // tail pixels per resident lane (PT_WF_TAIL_PX; round 2 re-sweep after the
+                                    // shading-pass fetch merges: C3 0.75 -> 1.5 +4.7%, the 1/2 shard +8%)
     int64_t wf_tail_npix = -1;      // explicit number of tail pixel slots (PT_WF_TAIL_NPIX), -1 = by wf_tail_px
     int wf_mid_chunks = -1;         // split shards: chunks of all but the last pixels (PT_WF_MID_CHUNKS;
                                     // -1 = automatic, 0 or 1 = one split for all)
@@ -2306,7 +2307,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 if (c->wf_fine_chunks > 0) chunks = (uint32_t)c->wf_fine_chunks;
             }
         } else if (c->wf_tail_chunks > 1) {
-            // (measured on C3: +6% with 0.5..1 tail pixel per lane in 4..8 chunks; 0.75 x 6)
+            // (measured on C3: +6% with 0.5..1 tail pixel per lane in 4..8 chunks, 0.75 x 6 in round 1;
+            // 1.5 x 6 since the shading pass's fetches were merged)
             chunks = (uint32_t)c->wf_tail_chunks;
             ntail = (uint32_t)std::min<uint64_t>(b.npix, (uint64_t)(c->wf_tail_px * (double)lanes));
         }
