@@ -2290,10 +2290,10 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             chunks = (uint32_t)c->wf_chunks;
             ntail = b.npix;
         } else if (2 * (uint64_t)b.npix < 5 * lanes) {
-            // ~16 fine units per lane, at most 12 chunks per pixel (round 2, after the shading pass got
-            // cheaper: the 1/8 C3 shard +4..5% with 10..12 chunks instead of 21 and 4 mid chunks
-            // instead of 6; the 1/4 shard's 11 unchanged)
-            chunks = (uint32_t)std::min<uint64_t>((16 * lanes + b.npix - 1) / b.npix, 12);
+            // ~16 fine units per lane, at most 8 chunks per pixel (round 2, after the shading pass got
+            // cheaper: the 1/8 C3 shard +5..6% with 8 chunks instead of 21 and 4 mid chunks instead of
+            // 6, profiles/r02_s4_units; the 1/4 shard alike with 8 or 11)
+            chunks = (uint32_t)std::min<uint64_t>((16 * lanes + b.npix - 1) / b.npix, 8);
             ntail = b.npix;
             // longer units first, the finer split for the last wf_fine_px pixels per lane
             // (measured on C3 shards: 1/4 shard 3 mid chunks, 1/8 shard 6: +3..4% over one split)
