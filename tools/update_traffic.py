@@ -38,9 +38,13 @@ out = {
 }
 if "GRBM_GUI_ACTIVE" in c:
     cyc = c["GRBM_GUI_ACTIVE"] / 8.0     # summed over the 8 XCDs
-    b = {"limiter": "valu+vmem-issue", "cycles_per_launch": int(cyc)}
+    b = {"limiter": "dependent memory round trips per walk step and shading pass (DESIGN.md 6); "
+                    "VALU issue and TD busy near their nominal rates",
+         "cycles_per_launch": int(cyc)}
     if "SQ_INSTS_VALU" in c:
-        b["valu_frac"] = round(c["SQ_INSTS_VALU"] * 4 / (1024 * cyc), 4)   # wave64 VALU op = 4 SIMD cycles
+        # wave64 VALU instructions per SIMD-cycle; the nominal rate is 0.25 (4 cycles per wave64 op),
+        # packed / dual-issued ops can take it above that
+        b["valu_insts_per_simd_cycle"] = round(c["SQ_INSTS_VALU"] / (1024 * cyc), 4)
     if "TD_TD_BUSY_sum" in c:
         b["td_busy"] = round(c["TD_TD_BUSY_sum"] / 256 / cyc, 4)
     if "TA_TA_BUSY_sum" in c:
