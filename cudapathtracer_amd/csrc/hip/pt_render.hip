@@ -1196,7 +1196,9 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     R.std_(CW_M, m0); R.st4(CW_M + 2, dlo(m1), dhi(m1), dlo(m2), dhi(m2));
                 } else {
                     // split pixel: keep L_n, finalize_pixels forms the ordered mean
-                    double* L = a.lbuf + ((size_t)R.ld(CW_Q) * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
+                    // (the slot is cell 8's last word, fetched with this sample's end: no dependent fetch
+                    // before the stores)
+                    double* L = a.lbuf + ((size_t)c8.w * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
                     L[0] = acc.r;
                     L[1] = acc.g;
                     L[2] = acc.b;
