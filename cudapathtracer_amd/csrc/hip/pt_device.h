@@ -757,6 +757,81 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
     return e;
 }
 
+// One BVH4 node visit on the loaded node (planes, child words): the four box tests, the entered
+// leaves queued as one entry, the entered inner children pushed far-to-near, the nearest one next.
+template <bool kCount>
+__device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX, const float4& NY, const float4& FY,
+                                       const float4& NZ, const float4& FZ, const uint4& ch, const Stack4& S,
+                                       float cull_rel, uint32_t node_mask, Counters& cnt)
+{
+    const float lim = w.best_t * cull_rel;
+    // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
+    float t0, t1, t2, t3;
+    bool e0, e1, e2, e3;
+    box_enter2(w, f2{NX.x, NX.y}, f2{NY.x, NY.y}, f2{NZ.x, NZ.y}, f2{FX.x, FX.y}, f2{FY.x, FY.y}, f2{FZ.x, FZ.y},
+               lim, t0, t1, e0, e1);
+    box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
+               lim, t2, t3, e2, e3);
+    uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
+    // entered leaf children as one queue entry: the node's leaf triangles have consecutive
+    // slots from its first (leaf children come first; each leaf child's word carries its slot
+    // bits), so the entry is that slot and an 8-bit mask
+    // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
+    const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
+    // a leaf child's word is kLeaf | first slot << kLeafBits | its slot bits, the first slot
+    // being the node's for all its leaf children: the OR of the entered leaf children's words
+    // is the queue entry (with kLeaf set)
+    const uint32_t lw = (e0 && l0 ? r0 : 0u) | (e1 && l1 ? r1 : 0u) | (e2 && l2 ? r2 : 0u) | (e3 && l3 ? r3 : 0u);
+    if ((lw & ((1u << kLeafBits) - 1u)) != 0u) {
+        const uint32_t e = lw & ~kLeaf;
+        if (!leaf4_pending(w)) w.leaf = e;
+        else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
+    }
+    // inner children, nearest first.  Each entered inner child becomes its stack entry (entry
+    // distance, >= 0, truncated to the bits above node_mask | node index): non-negative floats
+    // order like their bit patterns, so four u32 min/max pairs sort the entries by distance;
+    // leaves and boxes not entered become ~0 and sort last.
+    auto key = [&](float t, uint32_t r, bool e, bool l) -> uint32_t {
+        return (e && !l) ? ((__float_as_uint(t) & ~node_mask) | r) : kNone;
+    };
+    uint32_t k0 = key(t0, r0, e0, l0), k1 = key(t1, r1, e1, l1), k2 = key(t2, r2, e2, l2), k3 = key(t3, r3, e3, l3);
+    auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };
+    ksort(k0, k1); ksort(k2, k3); ksort(k0, k2); ksort(k1, k3); ksort(k1, k2);
+    if (__ballot(w.sp > kRing - 3) == 0ull) {
+        // no ring wrap-around possible in this wave: the valid keys (a sorted prefix) go to
+        // slots sp.. far-to-near with three unconditional writes (the slots above the new top
+        // are free)
+        const bool v1 = k1 != kNone, v2 = k2 != kNone, v3 = k3 != kNone;
+        uint32_t* const top = S.ring + w.sp * 64;
+        top[0] = v3 ? k3 : (v2 ? k2 : k1);
+        top[64] = v3 ? k2 : k1;
+        top[128] = k1;
+        w.sp += (int)v1 + (int)v2 + (int)v3;
+    } else {
+        if (k3 != kNone) push4<kCount>(w, S, k3, cnt);
+        if (k2 != kNone) push4<kCount>(w, S, k2, cnt);
+        if (k1 != kNone) push4<kCount>(w, S, k1, cnt);
+    }
+    w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
+}
+// After a step: take the next queued leaf entry when the pending one is done, and pop the next stack
+// entry not culled by the best hit when there is no node to visit.
+__device__ __forceinline__ void advance4(W4& w, const Stack4& S, float cull_rel, uint32_t node_mask)
+{
+    if (!leaf4_pending(w) && w.lsp > 0) {
+        --w.lsp;
+        w.leaf = S.ring[(kRing + w.lsp) * 64];
+    }
+    if (w.node == kNone) {
+        while (w.sp > 0) {
+            const uint32_t e = pop4(w, S);
+            if (__uint_as_float(e & ~node_mask) > w.best_t * cull_rel) continue;
+            w.node = e & node_mask;
+            break;
+        }
+    }
+}
+
 // One walk step.  Returns true while the walk continues.
 // A step fetches the next node AND the next pending leaf triangle in one memory round trip, tests
 // the triangle, then the node's four child boxes; entered leaf children are queued (tested in
@@ -834,72 +909,29 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         }
         w.leaf &= w.leaf - 1u;   // that leaf is done
     }
-    if (visit) {
-        const float lim = w.best_t * cull_rel;
-        // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
-        float t0, t1, t2, t3;
-        bool e0, e1, e2, e3;
-        box_enter2(w, f2{NX.x, NX.y}, f2{NY.x, NY.y}, f2{NZ.x, NZ.y}, f2{FX.x, FX.y}, f2{FY.x, FY.y}, f2{FZ.x, FZ.y},
-                   lim, t0, t1, e0, e1);
-        box_enter2(w, f2{NX.z, NX.w}, f2{NY.z, NY.w}, f2{NZ.z, NZ.w}, f2{FX.z, FX.w}, f2{FY.z, FY.w}, f2{FZ.z, FZ.w},
-                   lim, t2, t3, e2, e3);
-        uint32_t r0 = ch.x, r1 = ch.y, r2 = ch.z, r3 = ch.w;
-        // entered leaf children as one queue entry: the node's leaf triangles have consecutive
-        // slots from its first (leaf children come first; each leaf child's word carries its slot
-        // bits), so the entry is that slot and an 8-bit mask
-        // (ek: child k entered, lk: child k is a leaf; both also select the stack keys below)
-        const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0, l2 = (int32_t)r2 < 0, l3 = (int32_t)r3 < 0;
-        // a leaf child's word is kLeaf | first slot << kLeafBits | its slot bits, the first slot
-        // being the node's for all its leaf children: the OR of the entered leaf children's words
-        // is the queue entry (with kLeaf set)
-        const uint32_t lw = (e0 && l0 ? r0 : 0u) | (e1 && l1 ? r1 : 0u) | (e2 && l2 ? r2 : 0u) | (e3 && l3 ? r3 : 0u);
-        if ((lw & ((1u << kLeafBits) - 1u)) != 0u) {
-            const uint32_t e = lw & ~kLeaf;
-            if (!leaf4_pending(w)) w.leaf = e;
-            else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
-        }
-        // inner children, nearest first.  Each entered inner child becomes its stack entry (entry
-        // distance, >= 0, truncated to the bits above node_mask | node index): non-negative floats
-        // order like their bit patterns, so four u32 min/max pairs sort the entries by distance;
-        // leaves and boxes not entered become ~0 and sort last.
-        auto key = [&](float t, uint32_t r, bool e, bool l) -> uint32_t {
-            return (e && !l) ? ((__float_as_uint(t) & ~node_mask) | r) : kNone;
-        };
-        uint32_t k0 = key(t0, r0, e0, l0), k1 = key(t1, r1, e1, l1), k2 = key(t2, r2, e2, l2), k3 = key(t3, r3, e3, l3);
-        auto ksort = [](uint32_t& a, uint32_t& b) { const uint32_t lo = min(a, b); b = max(a, b); a = lo; };
-        ksort(k0, k1); ksort(k2, k3); ksort(k0, k2); ksort(k1, k3); ksort(k1, k2);
-        if (__ballot(w.sp > kRing - 3) == 0ull) {
-            // no ring wrap-around possible in this wave: the valid keys (a sorted prefix) go to
-            // slots sp.. far-to-near with three unconditional writes (the slots above the new top
-            // are free)
-            const bool v1 = k1 != kNone, v2 = k2 != kNone, v3 = k3 != kNone;
-            uint32_t* const top = S.ring + w.sp * 64;
-            top[0] = v3 ? k3 : (v2 ? k2 : k1);
-            top[64] = v3 ? k2 : k1;
-            top[128] = k1;
-            w.sp += (int)v1 + (int)v2 + (int)v3;
-        } else {
-            if (k3 != kNone) push4<kCount>(w, S, k3, cnt);
-            if (k2 != kNone) push4<kCount>(w, S, k2, cnt);
-            if (k1 != kNone) push4<kCount>(w, S, k1, cnt);
-        }
-        w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
-    }
-    if (!leaf4_pending(w) && w.lsp > 0) {
-        --w.lsp;
-        w.leaf = S.ring[(kRing + w.lsp) * 64];
-    }
-    if (w.node == kNone) {
-        while (w.sp > 0) {
-            const uint32_t e = pop4(w, S);
-            if (__uint_as_float(e & ~node_mask) > w.best_t * cull_rel) continue;
-            w.node = e & node_mask;
-            break;
-        }
-    }
+    if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
+    advance4(w, S, cull_rel, node_mask);
     return w.node != kNone || leaf4_pending(w);
 }
 #pragma clang diagnostic pop
+
+// The walk's first step for a ray just begun (walk4_begin passed): the root's visit from the LDS top
+// (no leaf can be pending yet), run where the ray is set up -- in the shading pass, where the lanes
+// beginning traces do it together -- instead of as a walk-phase step.  Returns true while the walk
+// continues (false: nothing entered, the ray misses).
+template <bool kCount>
+__device__ __forceinline__ bool walk4_root(W4& w, const Stack4& S, float cull_rel, uint32_t node_mask, Counters& cnt)
+{
+    const uint32_t mb = lds_addr(S.top);   // node 0
+    const float4 NX = lds_f4a(mb + w.nx), FX = lds_f4a(vsub_u32(mb, w.nx) + 48u);
+    const float4 NY = lds_f4a(mb + w.ny), FY = lds_f4a(vsub_u32(mb, w.ny) + 80u);
+    const float4 NZ = lds_f4a(mb + w.nz), FZ = lds_f4a(vsub_u32(mb, w.nz) + 112u);
+    const uint4 ch = lds_u4a(mb + 96u);
+    if (kCount) { ++cnt.nodes; ++cnt.top; }
+    visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
+    advance4(w, S, cull_rel, node_mask);
+    return w.node != kNone || leaf4_pending(w);
+}
 
 // Exact walk for the rare rays the fast path does not take (outside the Markstein
 // preconditions, or a BVH4 winner the reference would not have tested): the culled near-first

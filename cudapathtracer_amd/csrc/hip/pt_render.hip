@@ -60,6 +60,7 @@ struct Args {
     uint32_t wf_iters;              // shading iterations a lane may run per pass before yielding
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
     uint32_t top_nodes;             // wavefront kernel: BVH4 nodes 0..top_nodes-1 staged in LDS
+    uint32_t root_first;            // wavefront kernel: a new ray's root visit in the shading pass (begin_trace)
     uint32_t tile_fast4;            // tile kernel: trace with the render-path BVH4 walk (winner check, exact
                                     // slow walk as fallback) instead of the reference-BVH culled walk
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
@@ -915,7 +916,8 @@ __device__ __forceinline__ const Args& kernel_args_opaque()
 template <bool kCount>
 __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
                                            int32_t& htri, float& ht, W4& w, const Stack4& S,
-                                           unsigned long long* lcnt, const uint32_t* lprobe, uint32_t* done_rel)
+                                           unsigned long long* lcnt, const uint32_t* lprobe, uint32_t* done_rel,
+                                           Counters& cnt)
 {
     (void)a_in;
     const Args& a = kernel_args_opaque();
@@ -1316,6 +1318,12 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
       if (__ballot(again) == 0ull) break;
     }
 
+    // the root's visit of every ray begun in this pass, here -- all such lanes together, one copy of
+    // the code -- instead of as a walk step: the walk is one step shorter per ray.  (A fresh walk is
+    // the only one at node 0.)  Nothing entered: the walk is over without a candidate, as a finished
+    // walk would be; the lane shades in the next pass.
+    if (a.root_first && state == ST_TRACE && w.node == 0u && !walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt))
+        state = (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
     SEC(SEC_RECORD);
     R.st4(CW_N, (uint32_t)n, (uint32_t)i, fl, rng.d);
     R.st4(CW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
@@ -1433,7 +1441,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         if (kCount) ++shade_slots;
         // (the lane id is recomputed for the shading pass: one VGPR less live across the walk loop)
         if (state != ST_TRACE && state != ST_DONE)
-            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel);
+            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel, cnt);
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
@@ -1676,6 +1684,7 @@ struct pt_ctx {
     bool scene_fast = false;
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
+    uint32_t wf_root_first = 1;     // a new ray's root visit in the shading pass (PT_WF_ROOT_FIRST)
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
@@ -1891,6 +1900,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         while ((1u << bits) < nn) ++bits;
         c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_WF_ROOT_FIRST")) c->wf_root_first = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_JUMP_BYTES")) c->use_jump_bytes = atoi(e) != 0;
         if (const char* e = getenv("PT_TILE_FAST4")) c->tile_fast4 = atoi(e) != 0;
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
@@ -2238,6 +2248,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.nunits = a.ntiles_shard * 64u;
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
+    a.root_first = c->wf_root_first;
     a.wf_iters = c->wf_iters;
     a.node_mask = c->node_mask;
     a.nodes4 = c->nodes4;
