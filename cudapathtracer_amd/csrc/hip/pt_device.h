@@ -922,7 +922,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
 template <bool kCount>
 __device__ __forceinline__ bool walk4_root(W4& w, const Stack4& S, float cull_rel, uint32_t node_mask, Counters& cnt)
 {
-    const uint32_t mb = lds_addr(S.top);   // node 0
+    const uint32_t mb = lds_addr(S.top) + __umul24(w.node, kTopNodeBytes);   // node 0 (or a staged node: walk4_top)
     const float4 NX = lds_f4a(mb + w.nx), FX = lds_f4a(vsub_u32(mb, w.nx) + 48u);
     const float4 NY = lds_f4a(mb + w.ny), FY = lds_f4a(vsub_u32(mb, w.ny) + 80u);
     const float4 NZ = lds_f4a(mb + w.nz), FZ = lds_f4a(vsub_u32(mb, w.nz) + 112u);

@@ -1318,12 +1318,18 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
       if (__ballot(again) == 0ull) break;
     }
 
-    // the root's visit of every ray begun in this pass, here -- all such lanes together, one copy of
-    // the code -- instead of as a walk step: the walk is one step shorter per ray.  (A fresh walk is
-    // the only one at node 0.)  Nothing entered: the walk is over without a candidate, as a finished
-    // walk would be; the lane shades in the next pass.
-    if (a.root_first && state == ST_TRACE && w.node == 0u && !walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt))
-        state = (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
+    // the first visits of every ray begun in this pass (the root and, while the next node is staged
+    // in LDS and no leaf is queued, up to root_first - 1 more), here -- all such lanes together, one
+    // copy of the code -- instead of as walk steps: the walk is that many steps shorter per ray.  (A
+    // fresh walk is the only one at node 0.)  Nothing entered: the walk is over without a candidate,
+    // as a finished walk would be; the lane shades in the next pass.
+    if (a.root_first && state == ST_TRACE && w.node == 0u) {
+        bool more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        // (up to root_first visits: the next node too while it is staged in LDS and no leaf is queued)
+        for (uint32_t k = 1; more && k < a.root_first && w.node < S.ntop && !leaf4_pending(w); ++k)
+            more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        if (!more) state = (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
+    }
     SEC(SEC_RECORD);
     R.st4(CW_N, (uint32_t)n, (uint32_t)i, fl, rng.d);
     R.st4(CW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
@@ -1684,7 +1690,8 @@ struct pt_ctx {
     bool scene_fast = false;
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
-    uint32_t wf_root_first = 1;     // a new ray's root visit in the shading pass (PT_WF_ROOT_FIRST)
+    uint32_t wf_root_first = 4;     // a new ray's first visits (root + up to 3 staged nodes) in the shading pass
+                                    // (PT_WF_ROOT_FIRST; C3 1/2/3/4/6: 5331/5417/5461/5509/5406)
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
