@@ -61,6 +61,7 @@ struct Args {
     uint32_t node_mask;             // low bits of a packed stack entry holding the node index
     uint32_t top_nodes;             // wavefront kernel: BVH4 nodes 0..top_nodes-1 staged in LDS
     uint32_t root_first;            // wavefront kernel: a new ray's root visit in the shading pass (begin_trace)
+    uint32_t unit_queues;           // wavefront kernel: units dealt from kQueues counters (> 1) or one
     uint32_t tile_fast4;            // tile kernel: trace with the render-path BVH4 walk (winner check, exact
                                     // slow walk as fallback) instead of the reference-BVH culled walk
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
@@ -676,6 +677,10 @@ __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hi
 // Per-unit words of init_pixel_states' output beyond the XORWOW state (words 0..5: v0..v4, d)
 enum : uint32_t { UW_PXY = 6, UW_N0, UW_NEND, UW_TQ, UW_CD, kUnitWords = UW_CD + 3 };
 constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the image
+constexpr uint32_t kNoUnit = 0xffffffffu;
+constexpr uint32_t kQueues = 8;              // unit counters (Args::unit_queues > 1)
+constexpr uint32_t kQueueBlock = 64;         // units per block of a counter's class
+constexpr uint32_t kQueueStride = 32;        // words between the counters (one 128-B line each)
 constexpr uint32_t kMaxProbeEmitters = 4;    // last-bounce light probe: at most this many emissive triangles
 // LDS of a wavefront block after the counters: the probe's emitter count (16 B) and records, then the
 // staged BVH4 top nodes
@@ -1257,16 +1262,48 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
           continue;
       }
     // refill: lanes whose unit is finished take the next units of this shard
-    const uint64_t idle = __ballot(state == ST_IDLE);
+    uint64_t idle = __ballot(state == ST_IDLE);
     if (idle) {
         SEC(SEC_REFILL);
-        const uint32_t need = (uint32_t)__popcll(idle);
-        const int leader = __ffsll((long long)idle) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(a.pixel_counter, need);
-        base = __shfl(base, leader, 64);
+        uint32_t u = kNoUnit;
+        if (a.unit_queues > 1u) {
+            // The units dealt from kQueues counters (one 128-B line each), counter x owning the blocks
+            // j = x (mod kQueues) of kQueueBlock units in order -- so the unit sequence is still taken
+            // roughly front to back -- each wave starting at its block's counter and moving on when
+            // that one is exhausted (the block's LDS mask, so every wave of the block and every lane
+            // sees the same): the refill's atomics spread over kQueues addresses.  Which units a lane
+            // gets never changes what it computes.
+            uint32_t qdone = *reinterpret_cast<volatile const uint32_t*>(lprobe + 1);
+            const uint32_t x0 = blockIdx.x & (kQueues - 1u);
+            for (uint32_t r = 0; r < kQueues && idle && qdone != (1u << kQueues) - 1u; ++r) {
+                const uint32_t x = (x0 + r) & (kQueues - 1u);
+                if (qdone & (1u << x)) continue;
+                const int leader = __ffsll((long long)idle) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(a.pixel_counter + kQueueStride * (x + 1u), (uint32_t)__popcll(idle));
+                base = __shfl(base, leader, 64);
+                if (state == ST_IDLE && u == kNoUnit) {
+                    const uint32_t k = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                    const uint64_t uq = ((uint64_t)(k / kQueueBlock) * kQueues + x) * kQueueBlock + (k % kQueueBlock);
+                    if (uq < a.nunits) u = (uint32_t)uq;
+                }
+                const uint64_t left = __ballot(state == ST_IDLE && u == kNoUnit);
+                if (left) {   // (a counter only grows: past its class's end for good)
+                    qdone |= 1u << x;
+                    if (lane == leader) atomicOr(const_cast<uint32_t*>(lprobe + 1), 1u << x);
+                }
+                idle = left;
+            }
+            if (state == ST_IDLE && u == kNoUnit) u = a.nunits;   // every counter exhausted
+        } else {
+            const uint32_t need = (uint32_t)__popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.pixel_counter, need);
+            base = __shfl(base, leader, 64);
+            if (state == ST_IDLE) u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+        }
         if (state == ST_IDLE) {
-            const uint32_t u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             if (u >= a.nunits) {
                 if (kCount) {   // queue drained; this lane's end after it and since the start (binned at the end)
                     const unsigned long long now = wall_clock64();
@@ -1379,7 +1416,7 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     S.off_shift = 2;
     // the light probe's emitters (count, then records), then the top of the BVH4 (kTopNodeBytes per node)
     uint32_t* const lprobe = reinterpret_cast<uint32_t*>(lcnt + 4 + (kSections + kHist) / 2);
-    if (threadIdx.x == 0) lprobe[0] = a.num_emis;
+    if (threadIdx.x == 0) { lprobe[0] = a.num_emis; lprobe[1] = 0u; }   // ([1]: the refill's exhausted unit counters)
     if (a.num_lights < kLdsLights)
         for (uint32_t k = threadIdx.x; k < (a.num_lights + 1) * 3; k += blockDim.x)
             reinterpret_cast<float4*>(lprobe + 4 + kMaxProbeEmitters * 12)[k] = reinterpret_cast<const float4*>(a.lights)[k];
@@ -1690,6 +1727,7 @@ struct pt_ctx {
     bool scene_fast = false;
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
+    uint32_t wf_queues = kQueues;   // unit counters (PT_WF_QUEUES=1: one; 8: the 1/8 shard +5.8%, C3 +1.2%)
     uint32_t wf_root_first = 4;     // a new ray's first visits (root + up to 3 staged nodes) in the shading pass
                                     // (PT_WF_ROOT_FIRST; C3 1/2/3/4/6: 5331/5417/5461/5509/5406)
     uint32_t wf_waves_per_cu = 16;
@@ -1908,6 +1946,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->node_mask = (bits >= 31) ? 0x7fffffffu : ((1u << bits) - 1u);
         if (const char* e = getenv("PT_WF_THRESHOLD")) c->wf_threshold = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_ROOT_FIRST")) c->wf_root_first = (uint32_t)atoi(e);
+        if (const char* e = getenv("PT_WF_QUEUES")) c->wf_queues = (atoi(e) > 1) ? kQueues : 1u;
         if (const char* e = getenv("PT_JUMP_BYTES")) c->use_jump_bytes = atoi(e) != 0;
         if (const char* e = getenv("PT_TILE_FAST4")) c->tile_fast4 = atoi(e) != 0;
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
@@ -2153,7 +2192,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     }
     if (hipMalloc(reinterpret_cast<void**>(&c->counters), kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), 16) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), kQueueStride * (kQueues + 1) * 4) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         pt_destroy(c);
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
@@ -2256,6 +2295,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
     a.root_first = c->wf_root_first;
+    a.unit_queues = c->wf_queues;
     a.wf_iters = c->wf_iters;
     a.node_mask = c->node_mask;
     a.nodes4 = c->nodes4;
@@ -2276,7 +2316,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         a.tri_counts = c->tri_counts;
     }
     HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
-    HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, 16, stream));
+    HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
     const uint32_t waves_per_cu = 16;
     uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
     if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
