@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Benchmark of the per-pixel path-integration hot path (BASELINE.json north star).
 
-Workload (config C3): the ~262K-triangle procedural Sponza-class STAND-IN (Sponza is absent
-from this container; PT_SPONZA_OBJ=<path> uses a real file), 1920x1080, 256 spp, 3 bounces,
-unidirectional integrator (kernel.cu:417-515), seed 1234.  One "step" = one full render of
-that image (all samples), inputs resident in HBM; for N GPUs each rank renders its interleaved
-8x8 tiles into a zero-filled fp32 framebuffer and rank 0 receives the RCCL sum (weak scaling
-of the per-GPU work is NOT used: total work per step is fixed, so scaling is "strong").
+Workload (config C3, the default and the headline): the ~262K-triangle procedural Sponza-class
+STAND-IN (Sponza is absent from this container; PT_SPONZA_OBJ=<path> uses a real file), 1920x1080,
+256 spp, 3 bounces, unidirectional integrator (kernel.cu:417-515), seed 1234.  One "step" = one
+full render of that image (all samples), inputs resident in HBM; for N GPUs each rank renders its
+interleaved 8x8 tiles into a zero-filled fp32 framebuffer and rank 0 receives the RCCL sum (weak
+scaling of the per-GPU work is NOT used: total work per step is fixed, so scaling is "strong").
+--config C2 (Cornell 1024x1024, 64 spp, depth 8) / C4 (C3 at 1024 spp) / C5 (stand-in 3840x2160,
+4096 spp, depth 16) measure the other BASELINE configs the same way; --integrator 1 the HEAD
+integrator (kernel.cu:217-415).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with:
   value      = Msamples/s, whole job (pixel samples per second)
@@ -73,11 +76,25 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def scene_path(cache_dir):
+# BASELINE.json configs as bench workloads: scene, image, spp, bounces
+CONFIGS = {
+    "C2": dict(scene="cornell", width=1024, height=1024, spp=64, bounces=8),
+    "C3": dict(scene="standin", width=1920, height=1080, spp=256, bounces=3),
+    "C4": dict(scene="standin", width=1920, height=1080, spp=1024, bounces=3),
+    "C5": dict(scene="standin", width=3840, height=2160, spp=4096, bounces=16),
+}
+
+
+def scene_path(cache_dir, kind="standin"):
+    from cudapathtracer_amd import scenes
+    if kind == "cornell":   # the build's Cornell box OBJ+MTL (ceiling light facing -y, kernel.cu:503)
+        p = os.path.join(cache_dir, "models", "cornell.obj")
+        if not os.path.exists(p):
+            scenes.write_cornell(cache_dir)
+        return p, os.path.dirname(p) + "/", "cornell (build-authored Cornell box mesh)"
     real = os.environ.get("PT_SPONZA_OBJ")
     if real:
         return real, os.path.dirname(real) + "/", "sponza (PT_SPONZA_OBJ)"
-    from cudapathtracer_amd import scenes
     p = os.path.join(cache_dir, "models", "sponza_standin.obj")
     if not os.path.exists(p):
         scenes.write_sponza_standin(cache_dir)
@@ -94,7 +111,7 @@ def load(path, mtl):
     return s
 
 
-def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
+def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s, integrator=0):
     """Oracle (CPU restatement of the same integrator) on a bounded subset of the same image."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -106,15 +123,15 @@ def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
     # calibrate on a spread of tiles, then size the subset (every k-th tile, full spp) to the budget
     cal_tiles = np.linspace(0, ntiles - 1, 4 * threads).astype(np.int64)
     t0 = time.time()
-    oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=shard.tile_pixels(width, height, cal_tiles),
-                  threads=threads)
+    oracle.render(osc, ocam, width, height, spp, bounces, integrator, 1234,
+                  pixels=shard.tile_pixels(width, height, cal_tiles), threads=threads)
     dt = max(time.time() - t0, 1e-3) / len(cal_tiles)
     tiles_fit = max(1, int(budget_s / dt))
     stride = max(1, ntiles // tiles_fit)
     tiles = np.arange(stride // 2, ntiles, stride)[:tiles_fit]
     pix = shard.tile_pixels(width, height, tiles)
     t0 = time.time()
-    _, cnt = oracle.render(osc, ocam, width, height, spp, bounces, 0, 1234, pixels=pix, threads=threads)
+    _, cnt = oracle.render(osc, ocam, width, height, spp, bounces, integrator, 1234, pixels=pix, threads=threads)
     dt = time.time() - t0
     samples = len(pix) * spp
     return {
@@ -124,6 +141,21 @@ def cpu_baseline(scene, cam_kw, width, height, spp, bounces, threads, budget_s):
         "sample": "%d pixels (every %d-th 8x8 tile) x %d spp of the same %dx%d image, %.1fs"
                   % (len(pix), stride, spp, width, height, dt),
     }
+
+
+def traffic_entry(path, cfg, sha):
+    """The profiles/traffic.json entry measured on this kernel source and bench config, or None.
+    The file holds {"entries": [...]}, one per (config, source hash)."""
+    if not os.path.exists(path):
+        return None
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for e in tj.get("entries", [tj] if "config" in tj else []):
+        if e.get("config") == cfg and e.get("kernel_source_sha256") == sha:
+            return e
+    return None
 
 
 def roofline(counts, kms, W, H, args, world):
@@ -143,8 +175,13 @@ def roofline(counts, kms, W, H, args, world):
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
             "traffic_source": None,
             "algorithmic_bytes_per_launch": int(alg), "algorithmic_gbs": round(alg / sec / 1e9, 2),
-            "kernel": "render_unidir_wf" if args.integrator == 0 and not (args.flags & 1) else "render_tiles",
-            "kernel_ms": round(kms, 3), "kernel_source_sha256": kernel_source_sha256(),
+            "kernel": KERNEL_NAME(args),
+            "kernel_ms": round(kms, 3),
+            "kernel_ms_note": "the integration kernel alone (HIP events around its launch on its stream), "
+                              "without the seeding pre-pass and the split-pixel finalisation",
+            "traffic_note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE: bytes between L2 and the memory side (Infinity "
+                            "Cache hits included), so frac is an upper bound on the HBM fraction",
+            "kernel_source_sha256": kernel_source_sha256(),
             "node_fetches": int(counts["node_tests"]), "lds_node_fetches": int(counts["lds_node_tests"]),
             "tri_tests": int(counts["tri_tests"]),
             "walk_simd_util": round(counts["node_tests"] / max(counts["walk_lane_slots"], 1), 4),
@@ -152,21 +189,17 @@ def roofline(counts, kms, W, H, args, world):
             "accel_fallbacks": int(counts["accel_fallbacks"]), "spill_entries": int(counts["spill_entries"]),
             "walk_phase_frac": round(counts["walk_cycles"] / max(counts["walk_cycles"] + counts["shade_cycles"], 1), 4),
             "shade_phases": int(counts["shade_lane_slots"] // 64)}
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-        except (OSError, ValueError):
-            tj = {}
-        if (tj.get("config") == [W, H, args.spp, args.bounces, args.integrator, max(world, args.sim_shards)]
-                and tj.get("kernel_source_sha256") == roof["kernel_source_sha256"]):
-            traffic = int(tj["traffic_bytes_per_launch"])
-            roof["traffic"] = traffic
-            roof["achieved"] = round(traffic / sec / 1e9, 2)
-            roof["frac"] = round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4)
-            roof["traffic_source"] = {"profile": tj.get("profile"), "method": tj.get("method"),
-                                      "kernel_ms_profiled": tj.get("kernel_ms")}
-            if tj.get("binding"):
-                roof["binding"] = tj["binding"]
+    tj = traffic_entry(args.traffic_json, [W, H, args.spp, args.bounces, args.integrator, max(world, args.sim_shards)],
+                       roof["kernel_source_sha256"])
+    if tj is not None:
+        traffic = int(tj["traffic_bytes_per_launch"])
+        roof["traffic"] = traffic
+        roof["achieved"] = round(traffic / sec / 1e9, 2)
+        roof["frac"] = round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4)
+        roof["traffic_source"] = {"profile": tj.get("profile"), "method": tj.get("method"),
+                                  "kernel_ms_profiled": tj.get("kernel_ms")}
+        if tj.get("binding"):
+            roof["binding"] = tj["binding"]
     return roof
 
 
@@ -223,15 +256,21 @@ def make_reduce(dist, backend, rank):
     return gloo_reduce
 
 
+def KERNEL_NAME(args):
+    return "render_unidir_wf" if not (args.flags & 1) else "render_tiles"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS),
+                    help="BASELINE config: scene, image size, spp and bounces (overridable below)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--bounces", type=int, default=None)
     ap.add_argument("--integrator", type=int, default=0)
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -243,6 +282,9 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
+    for k, v in CONFIGS[args.config].items():
+        if k != "scene" and getattr(args, k) is None:
+            setattr(args, k, v)
 
     import torch
     import torch.distributed as dist
@@ -270,9 +312,10 @@ def main():
             dist.init_process_group(backend)
 
     os.makedirs(args.cache_dir, exist_ok=True)
-    path, mtl, scene_name = scene_path(args.cache_dir)
+    kind = CONFIGS[args.config]["scene"]
+    path, mtl, scene_name = scene_path(args.cache_dir, kind)
     scene = load(path, mtl)
-    cam_kw = dict(scenes.SPONZA_STANDIN_CAMERA)
+    cam_kw = dict(scenes.CORNELL_CAMERA if kind == "cornell" else scenes.SPONZA_STANDIN_CAMERA)
     W, H = args.width, args.height
     cam = pt.make_camera(width=W, height=H, **cam_kw)
     r = pt.Renderer(scene, device=local)
@@ -327,7 +370,8 @@ def main():
         roof = roofline(counts, kms, W, H, args, world) if counts is not None else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget)
+            cpu = cpu_baseline(scene, cam_kw, W, H, args.spp, args.bounces, args.cpu_threads, args.cpu_budget,
+                               args.integrator)
         out = {
             "metric": "Mrays/sec + Msamples/sec, Sponza 1080p 256spp, 1/2/4/8 GPU",
             "value": round(samples / elapsed / 1e6, 3),
@@ -339,11 +383,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 geometry / f64 radiance",
             "data": "synthetic",
-            "config": {"workload": "C3 %s %dx%d %dspp %d bounces integrator=%d" % (
-                scene_name, W, H, args.spp, args.bounces, args.integrator),
+            "config": {"workload": "%s %s %dx%d %dspp %d bounces integrator=%d" % (
+                args.config, scene_name, W, H, args.spp, args.bounces, args.integrator),
                 "scene": scene_name, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "integrator": "unidirectional" if args.integrator == 0 else "head", "seed": 1234,
-                "parallelism": ("image tiles %dx, RCCL reduce" % world if distributed else
+                "parallelism": ("image tiles %dx, %s reduce" % (world, "RCCL" if backend == "nccl" else backend)
+                                if distributed else
                                 "1 GPU" if shards == 1 else "1 GPU rendering shard 0 of %d (diagnostic)" % shards)},
             "mrays_per_s_traced": round(traced / elapsed / 1e6, 3),
             "mrays_per_s_reference_equiv": round(refrays / elapsed / 1e6, 3),

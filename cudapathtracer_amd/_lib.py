@@ -22,8 +22,9 @@ PT_FLAG_NO_PRIMARY_CACHE = 0x4
 PT_FLAG_COUNT = 0x8
 PT_FLAG_REFERENCE_BVH = 0x10
 PT_FLAG_TRI_COUNTS = 0x20
+PT_ORDER_SCANLINE, PT_ORDER_MORTON = 0, 1
 PT_LIGHT_SPHERE = 0x80000000     # lights[] entry of an emissive sphere
-ABI_VERSION = 5                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
+ABI_VERSION = 6                 # PT_ABI_VERSION of include/pt/pt.h these bindings mirror
 PT_BVH_LEAF_FLAG = 0x80000000
 
 
@@ -63,7 +64,8 @@ class SceneView(C.Structure):
 class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("bounces", C.c_int32),
                 ("integrator", C.c_int32), ("flags", C.c_uint32), ("seed", C.c_uint64),
-                ("shard_index", C.c_int32), ("shard_count", C.c_int32)]
+                ("shard_index", C.c_int32), ("shard_count", C.c_int32), ("pixel_order", C.c_int32),
+                ("tile_w", C.c_int32), ("tile_h", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -72,7 +74,7 @@ class Stats(C.Structure):
                 ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("walk_lane_slots", C.c_uint64),
                 ("leaf_steps", C.c_uint64), ("shade_lane_slots", C.c_uint64), ("accel_fallbacks", C.c_uint64),
                 ("walk_cycles", C.c_uint64), ("shade_cycles", C.c_uint64), ("spill_entries", C.c_uint64),
-                ("lds_node_tests", C.c_uint64)]
+                ("lds_node_tests", C.c_uint64), ("work_units", C.c_uint64), ("split_pixels", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -98,6 +100,7 @@ SIGNATURES = {
                              C.POINTER(Vec3), C.POINTER(Vec3)]),
     "pt_write_ppm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_write_ppm_f64": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "pt_write_ppm_order": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "pt_tonemap_u8": (C.c_int, [C.c_double]),
     "pt_accel_digest": (C.c_int, [C.POINTER(SceneView), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_int32)]),
@@ -113,6 +116,8 @@ SIGNATURES = {
     "pt_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pt_write_ppm_codes": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     "pt_write_pfm": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    "pt_shard_pixels": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_uint32,
+                                  C.POINTER(C.c_uint32)]),
     "pt_group_create": (C.c_void_p, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_int)]),
     "pt_group_size": (C.c_int, [C.c_void_p]),
     "pt_render_group": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.POINTER(Stats)]),

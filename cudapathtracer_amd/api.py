@@ -143,9 +143,14 @@ def morton_i_to_pxl(i):
     return x.value, y.value
 
 
-def write_ppm(path, img):
-    """kernel.cu:763-778 on a (H, W, 3) float32 or float64 mean image."""
+def write_ppm(path, img, pixel_order=0, width=None, height=None):
+    """kernel.cu:763-778 on a (H, W, 3) float32 or float64 mean image, or on a Morton-ordered
+    (W*H, 3) float32 buffer (pixel_order=PT_ORDER_MORTON, width/height given)."""
     img = np.ascontiguousarray(img)
+    if pixel_order == L.PT_ORDER_MORTON:
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        L.check(L.lib().pt_write_ppm_order(str(path).encode(), img.ctypes.data, int(width), int(height), 1))
+        return
     h, w = img.shape[:2]
     if img.dtype == np.float64:
         L.check(L.lib().pt_write_ppm_f64(str(path).encode(), img.ctypes.data, w, h))
@@ -211,26 +216,36 @@ class Renderer:
             pass
 
     @staticmethod
-    def params(width, height, spp, bounces=3, integrator=0, seed=1234, flags=0, shard_index=0, shard_count=1):
+    def params(width, height, spp, bounces=3, integrator=0, seed=1234, flags=0, shard_index=0, shard_count=1,
+               pixel_order=0, tile_w=0, tile_h=0):
         p = L.Params()
         p.width, p.height, p.spp, p.bounces = int(width), int(height), int(spp), int(bounces)
         p.integrator, p.flags, p.seed = int(integrator), int(flags), int(seed)
         p.shard_index, p.shard_count = int(shard_index), int(shard_count)
+        p.pixel_order, p.tile_w, p.tile_h = int(pixel_order), int(tile_w), int(tile_h)
         return p
 
     def render(self, cam, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0,
-               shard_index=0, shard_count=1):
-        """Returns (image float32 (H, W, 3), stats dict)."""
-        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count)
-        out = np.zeros((height, width, 3), dtype=np.float32)
+               shard_index=0, shard_count=1, pixel_order=0, tile_w=0, tile_h=0, out=None):
+        """Returns (image float32, stats dict).  The image is (H, W, 3) in scanline order, or the
+        reference's Morton-indexed imgBuff (W*H, 3) with pixel_order=PT_ORDER_MORTON.  `out`: a
+        C-contiguous float32 array of W*H*3 values to render into (reused across frames)."""
+        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count,
+                        pixel_order, tile_w, tile_h)
+        shape = (height * width, 3) if pixel_order == L.PT_ORDER_MORTON else (height, width, 3)
+        if out is None:
+            out = np.zeros(shape, dtype=np.float32)
+        elif out.dtype != np.float32 or out.size != width * height * 3 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float32 array of W*H*3 values")
         st = L.Stats()
         L.check(L.lib().pt_render(self._h, C.byref(p), C.byref(cam), out.ctypes.data, C.byref(st)))
         return out, st.as_dict()
 
     def render_device(self, cam, d_out_ptr, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0,
-                      shard_index=0, shard_count=1, stream_ptr=None):
+                      shard_index=0, shard_count=1, stream_ptr=None, pixel_order=0, tile_w=0, tile_h=0):
         """Render this shard into a caller-owned, zero-filled device buffer (e.g. a torch tensor)."""
-        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count)
+        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count,
+                        pixel_order, tile_w, tile_h)
         st = L.Stats()
         L.check(L.lib().pt_render_device(self._h, C.byref(p), C.byref(cam), C.c_void_p(int(d_out_ptr)),
                                          None if stream_ptr is None else C.c_void_p(int(stream_ptr)), C.byref(st)))
@@ -314,10 +329,15 @@ class Group:
         except Exception:
             pass
 
-    def render(self, cam, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0):
-        """Returns (image float32 (H, W, 3), summed stats dict)."""
-        p = Renderer.params(width, height, spp, bounces, integrator, seed, flags)
-        out = np.zeros((height, width, 3), dtype=np.float32)
+    def render(self, cam, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0, pixel_order=0,
+               tile_w=0, tile_h=0, out=None):
+        """Returns (image float32 (H, W, 3) -- (W*H, 3) in Morton order --, summed stats dict)."""
+        p = Renderer.params(width, height, spp, bounces, integrator, seed, flags, 0, 1, pixel_order, tile_w, tile_h)
+        shape = (height * width, 3) if pixel_order == L.PT_ORDER_MORTON else (height, width, 3)
+        if out is None:
+            out = np.zeros(shape, dtype=np.float32)
+        elif out.dtype != np.float32 or out.size != width * height * 3 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float32 array of W*H*3 values")
         st = L.Stats()
         L.check(L.lib().pt_render_group(self._h, C.byref(p), C.byref(cam), out.ctypes.data, C.byref(st)))
         return out, st.as_dict()

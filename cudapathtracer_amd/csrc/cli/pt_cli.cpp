@@ -11,6 +11,8 @@
 //                                         --spp gives the sample count directly
 // --gpus N                                shard image tiles over devices 0..N-1 (pt_render_multi:
 //                                         one context per device, one RCCL reduce of the shards)
+// --morton                                render into the reference's Morton-indexed framebuffer
+//                                         (square power-of-two sizes); --tile WxH sets the shard tile
 // --tri-counts out.csv                    per-triangle test counts (the reference's out.csv,
 //                                         kernel.cu:742-750); --reference-walk makes them the
 //                                         reference's own (its exact trace() sequence)
@@ -40,7 +42,7 @@ struct Obj {
             "              [--width W] [--height H] [--spp N | --num-samples N] [--bounces D]\n"
             "              [--integrator unidir|head] [--seed S] [--cam X,Y,Z] [--dist D] [--focal F]\n"
             "              [--radius R] [--gpus N] [--out image.ppm] [--pfm image.pfm] [--quiet]\n"
-            "              [--tri-counts out.csv [--reference-walk]]\n");
+            "              [--tri-counts out.csv [--reference-walk]] [--morton] [--tile WxH]\n");
     exit(2);
 }
 
@@ -117,6 +119,10 @@ int main(int argc, char** argv)
         else if (a == "--quiet") quiet = true;
         else if (a == "--tri-counts") tri_csv = next();
         else if (a == "--reference-walk") ref_walk = true;
+        else if (a == "--morton") p.pixel_order = PT_ORDER_MORTON;   // the reference's imgBuff order
+        else if (a == "--tile") {
+            if (sscanf(next().c_str(), "%dx%d", &p.tile_w, &p.tile_h) != 2) usage("--tile is WxH");
+        }
         else if (a == "-h" || a == "--help") usage(nullptr);
         else usage(("unknown option " + a).c_str());
     }
@@ -178,10 +184,23 @@ int main(int argc, char** argv)
                "%.1f Mrays/s nominal (kernel.cu:757)\n",
                gpus, secs, samples / secs / 1e6, traced / secs / 1e6, reference / secs / 1e6, nominal / secs / 1e6);
     }
-    std::vector<int32_t> codes(n);
-    if (pt_tonemap(ctx[0], img.data(), p.width, p.height, codes.data()) != PT_OK) return die("tone map");
-    if (pt_write_ppm_codes(out.c_str(), codes.data(), p.width, p.height) != PT_OK) return die("write PPM");
-    if (!pfm.empty() && pt_write_pfm(pfm.c_str(), img.data(), p.width, p.height) != PT_OK) return die("write PFM");
+    if (p.pixel_order == PT_ORDER_MORTON) {
+        // the buffer as the reference holds it (imgBuff[mortonPxltoI(x,y)]): the PPM loop of
+        // kernel.cu:763-778 reads it through the Morton map
+        if (pt_write_ppm_order(out.c_str(), img.data(), p.width, p.height, PT_ORDER_MORTON) != PT_OK) return die("write PPM");
+        if (!pfm.empty()) {
+            std::vector<float> scan(n);
+            for (int y = 0; y < p.height; ++y)
+                for (int x = 0; x < p.width; ++x)
+                    memcpy(&scan[((size_t)y * p.width + x) * 3], &img[(size_t)pt_morton_pxl_to_i(x, y) * 3], 12);
+            if (pt_write_pfm(pfm.c_str(), scan.data(), p.width, p.height) != PT_OK) return die("write PFM");
+        }
+    } else {
+        std::vector<int32_t> codes(n);
+        if (pt_tonemap(ctx[0], img.data(), p.width, p.height, codes.data()) != PT_OK) return die("tone map");
+        if (pt_write_ppm_codes(out.c_str(), codes.data(), p.width, p.height) != PT_OK) return die("write PPM");
+        if (!pfm.empty() && pt_write_pfm(pfm.c_str(), img.data(), p.width, p.height) != PT_OK) return die("write PFM");
+    }
     for (pt_ctx* c : ctx) pt_destroy(c);
     pt_scene_free(s);
     return 0;

@@ -28,6 +28,8 @@ struct pt_group {
     std::vector<float*> fb;         // per device: its shard, zero elsewhere
     float* result = nullptr;        // on dev[0]: the reduced image
     size_t bytes = 0;               // current framebuffer size
+    void* pinned = nullptr;         // pinned staging buffer of the image copy-out (pt::copy_to_host)
+    size_t pinned_bytes = 0;
 };
 
 namespace {
@@ -60,12 +62,16 @@ void release(pt_group* g)
     g->comm.clear();
     g->result = nullptr;
     g->bytes = 0;
+    pt::free_pinned(g->pinned);
+    g->pinned = nullptr;
+    g->pinned_bytes = 0;
 }
 
 // (re)allocate the per-device framebuffers and device 0's result buffer for `bytes`
 int ensure_buffers(pt_group* g, size_t bytes)
 {
     if (g->bytes >= bytes) return PT_OK;
+    g->bytes = 0;   // (until every buffer below exists: a partial failure reallocates on the next call)
     for (size_t i = 0; i < g->dev.size(); ++i) {
         hipError_t e = hipSetDevice(g->dev[i]);
         if (e != hipSuccess) return hip_fail("hipSetDevice", e);
@@ -209,14 +215,16 @@ int pt_render_group(pt_group* g, const pt_params* params, const pt_camera* cam, 
         }
     }
     if ((r = ncclGroupEnd()) != ncclSuccess) return nccl_fail("ncclGroupEnd", r);
-    for (int i = 0; i < n; ++i) {
+    for (int i = 1; i < n; ++i) {
         hipError_t e = hipSetDevice(g->dev[i]);
         if (e == hipSuccess) e = hipStreamSynchronize(g->stream[i]);
         if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
     }
+    // the image leaves device 0 behind its reduce on the same stream: one DMA into pinned staging,
+    // then a parallel host copy into the caller's buffer (pt_render's path)
     hipError_t e = hipSetDevice(g->dev[0]);
-    if (e == hipSuccess) e = hipMemcpy(out_rgb, g->result, bytes, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail("hipMemcpy(result)", e);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    if (int rc0 = pt::copy_to_host(out_rgb, g->result, bytes, g->stream[0], &g->pinned, &g->pinned_bytes)) return rc0;
     if (stats) {
         pt_stats sum;
         memset(&sum, 0, sizeof(sum));

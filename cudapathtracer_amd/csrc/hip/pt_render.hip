@@ -15,6 +15,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../host/host_internal.h"
@@ -51,6 +52,9 @@ struct Args {
     uint64_t seed;
     int32_t shard_index, shard_count;
     uint32_t tiles_x, ntiles_shard;
+    uint32_t tile_w, tile_h;        // shard tile (multiples of 8): 8x8 blocks of 64 work slots, row-major
+    uint32_t tile_bx, tile_blocks;  // 8x8 blocks per tile row / per tile
+    uint32_t morton_out;            // PT_ORDER_MORTON: pixel (x,y) written at out[mortonPxltoI(x,y)*3]
     uint32_t stack_words;           // LDS words per wave
     float cull_rel, cull_abs;
     uint32_t* pixel_counter;        // wavefront kernel: next pixel unit
@@ -197,11 +201,14 @@ struct Tracer {
                         h.tri = (int32_t)__float_as_uint(C.y);
                         ok = ref_tested(__float_as_uint(C.w), o, d, a->rnodes, a->rparent);
                     }
-                    if (!ok)
+                    if (!ok) {
+                        atomicAdd(a->counters + 8, 1ull);   // (accel_fallbacks, as trace_rays counts them)
                         trace_slow(o, d, a->root, a->nodes, a->tris_leaf, S.spill(), S.stride, a->cull_rel, a->cull_abs,
                                    &h.tri, &h.t, cnt.tri_counts);
+                    }
                 }
                 } else {   // outside the Markstein preconditions: the exact slow walk
+                    atomicAdd(a->counters + 8, 1ull);
                     trace_slow(o, d, a->root, a->nodes, a->tris_leaf, S.spill(), S.stride, a->cull_rel, a->cull_abs,
                                &h.tri, &h.t, cnt.tri_counts);
                 }
@@ -515,6 +522,36 @@ __device__ __forceinline__ uint32_t morton2(uint32_t x, uint32_t y)   // camera.
     return r;
 }
 
+// Work slot q of this shard -> pixel: tile q / (tile_w*tile_h) of the shard (tile t = shard_index +
+// that * shard_count, row-major over the tile grid), 8x8 block ((q >> 6) mod tile_blocks) of the tile
+// (row-major), Morton order within the block -- 64 consecutive slots (a wave's lanes) are one 8x8
+// block.  False for a slot outside the image (partial tiles at the right / bottom edge).
+// (host and device: pt_shard_pixels exports the same mapping; T = Args or TileMap)
+template <typename T>
+__host__ __device__ __forceinline__ bool unit_pixel(const T& a, uint32_t q, uint32_t* px, uint32_t* py)
+{
+    const uint32_t k = q >> 6, l = q & 63u;
+    const uint32_t tl = (a.tile_blocks == 1u) ? k : k / a.tile_blocks;
+    const uint32_t b = k - tl * a.tile_blocks;
+    const uint32_t t = (uint32_t)a.shard_index + tl * (uint32_t)a.shard_count;
+    const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
+    const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
+    const uint32_t by = (a.tile_bx == 1u) ? b : b / a.tile_bx;
+    *px = (t % a.tiles_x) * a.tile_w + (b - by * a.tile_bx) * kTile + qx;
+    *py = (t / a.tiles_x) * a.tile_h + by * kTile + qy;
+    return *px < (uint32_t)a.w && *py < (uint32_t)a.h;
+}
+// the tile-map fields of Args, for the host
+struct TileMap {
+    int32_t w, h, shard_index, shard_count;
+    uint32_t tiles_x, tile_w, tile_h, tile_bx, tile_blocks;
+};
+// index of pixel (px, py) in the output buffer (pt_params.pixel_order)
+__device__ __forceinline__ size_t out_pixel(const Args& a, uint32_t px, uint32_t py)
+{
+    return a.morton_out ? (size_t)morton2(px, py) : (size_t)py * (size_t)a.w + px;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
 #pragma unroll
@@ -538,17 +575,13 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
     unsigned long long samples = 0;
     const bool skip_dead = !(a.flags & PT_FLAG_NO_DEAD_PATH_SKIP);
     const bool memo = !(a.flags & PT_FLAG_NO_PRIMARY_CACHE);
-    const uint32_t mx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4);
-    const uint32_t my = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
     for (;;) {
-        uint32_t k = 0;
+        uint32_t k = 0;   // the next 8x8 block of this shard's tiles (64 work slots)
         if (lane == 0) k = atomicAdd(a.tile_counter, 1u);
         k = __shfl(k, 0, 64);
-        if (k >= a.ntiles_shard) break;
-        const uint32_t t = (uint32_t)a.shard_index + k * (uint32_t)a.shard_count;
-        const uint32_t px = (t % a.tiles_x) * kTile + mx;
-        const uint32_t py = (t / a.tiles_x) * kTile + my;
-        if (px >= (uint32_t)a.w || py >= (uint32_t)a.h) continue;
+        if (k >= a.ntiles_shard * a.tile_blocks) break;
+        uint32_t px, py;
+        if (!unit_pixel(a, k * 64u + (uint32_t)lane, &px, &py)) continue;
         const uint32_t idx = morton2(px, py);
         Rng rng;
         rng_init(rng, a.seed, idx, a.jump);
@@ -569,7 +602,7 @@ __global__ __launch_bounds__(64) void render_tiles(Args a)
             m2 = (m2 * fn1) / fn + L.b / fn;
         }
         samples += (unsigned long long)a.spp;
-        float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+        float* o3 = a.out + out_pixel(a, px, py) * 3;
         o3[0] = (float)m0;
         o3[1] = (float)m1;
         o3[2] = (float)m2;
@@ -691,16 +724,6 @@ constexpr uint32_t kProbeLdsBytes = 16 + kMaxProbeEmitters * (uint32_t)sizeof(DT
 __device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c, uint32_t chunks)
 {
     return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / chunks);
-}
-__device__ __forceinline__ bool unit_pixel(const Args& a, uint32_t q, uint32_t* px, uint32_t* py)
-{
-    const uint32_t t = (uint32_t)a.shard_index + (q >> 6) * (uint32_t)a.shard_count;
-    const uint32_t l = q & 63u;
-    const uint32_t qx = (l & 1) | ((l >> 1) & 2) | ((l >> 2) & 4);
-    const uint32_t qy = ((l >> 1) & 1) | ((l >> 2) & 2) | ((l >> 3) & 4);
-    *px = (t % a.tiles_x) * kTile + qx;
-    *py = (t / a.tiles_x) * kTile + qy;
-    return *px < (uint32_t)a.w && *py < (uint32_t)a.h;
 }
 
 // The XORWOW draws one sample of radianceAlongSingleStep2 consumes, without tracing: the count
@@ -829,7 +852,7 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     if (t >= a.ntail) return;
     uint32_t px, py;
     if (!unit_pixel(a, a.nwhole + t, &px, &py)) return;
-    const size_t pix = (size_t)py * (size_t)a.w + px;
+    const size_t pix = out_pixel(a, px, py);
     const double* L = a.lbuf + (size_t)t * a.spp * 3;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
     // one sample: the six quotients by fn as one IEEE reciprocal + Markstein corrections (RN(x/fn)
@@ -1193,7 +1216,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                         m2 = x2 / fn + acc.b / fn;
                     }
                     if (n >= a.spp) {
-                        float* o3 = a.out + ((size_t)py * (size_t)a.w + px) * 3;
+                        float* o3 = a.out + out_pixel(a, px, py) * 3;
                         o3[0] = (float)m0;
                         o3[1] = (float)m1;
                         o3[2] = (float)m2;
@@ -1600,6 +1623,7 @@ __global__ __launch_bounds__(256) void trace_rays(Args a, const float* __restric
             const Hit h = trace_reference<kCount>(o, d, a.rnodes, a.tris_orig, wave_lds, lane, cnt);
             htri = h.tri; ht = h.t;
         } else if (!((a.scene_fast != 0u) && ray_fast(o, d))) {
+            atomicAdd(a.counters + 8, 1ull);
             trace_slow(o, d, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs, &htri, &ht,
                        cnt.tri_counts);
         } else {
@@ -1726,7 +1750,10 @@ struct pt_ctx {
     int32_t depth = 0;
     uint32_t num_tris = 0;
     float scene_extent = 1.0f;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    void* pinned = nullptr;                    // pt_render: pinned staging buffer of the image copy-out
+    size_t pinned_bytes = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the whole render
+    hipEvent_t ek0 = nullptr, ek1 = nullptr;   // the integration kernel alone
     int num_cus = 256;
     uint32_t* pixel_counter = nullptr;
     bool scene_fast = false;
@@ -2198,7 +2225,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if (hipMalloc(reinterpret_cast<void**>(&c->counters), kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), kQueueStride * (kQueues + 1) * 4) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ek0) != hipSuccess || hipEventCreate(&c->ek1) != hipSuccess) {
         pt_destroy(c);
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
     }
@@ -2217,8 +2245,11 @@ void pt_destroy(pt_ctx* c)
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    pt::free_pinned(c->pinned);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ek0) (void)hipEventDestroy(c->ek0);
+    if (c->ek1) (void)hipEventDestroy(c->ek1);
     delete c;
 }
 
@@ -2264,6 +2295,14 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     if (p->shard_count < 1 || p->shard_index < 0 || p->shard_index >= p->shard_count)
         return pt::fail(PT_E_INVALID, "pt_render: shard %d of %d", p->shard_index, p->shard_count);
     if (cam->pxl_width <= 0 || cam->pxl_height <= 0) return pt::fail(PT_E_INVALID, "pt_render: camera pixel size must be > 0");
+    if (p->pixel_order != PT_ORDER_SCANLINE && p->pixel_order != PT_ORDER_MORTON)
+        return pt::fail(PT_E_INVALID, "pt_render: unknown pixel order %d", p->pixel_order);
+    if (p->pixel_order == PT_ORDER_MORTON && !pt::morton_size_ok(p->width, p->height))
+        return pt::fail(PT_E_INVALID, "pt_render: Morton pixel order needs a square power-of-two image, not %dx%d "
+                        "(the reference's imgBuff indexing, kernel.cu:543,771)", p->width, p->height);
+    for (const int32_t v : {p->tile_w, p->tile_h})
+        if (v != 0 && (v < 8 || v > 256 || v % 8 != 0))
+            return pt::fail(PT_E_INVALID, "pt_render: tile size %dx%d (0 = 8, else multiples of 8 up to 256)", p->tile_w, p->tile_h);
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
 
@@ -2282,9 +2321,13 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     a.cam.w = cam->pxl_width; a.cam.h = cam->pxl_height;
     a.w = p->width; a.h = p->height; a.spp = p->spp; a.bounces = p->bounces; a.flags = p->flags; a.seed = p->seed;
     a.shard_index = p->shard_index; a.shard_count = p->shard_count;
-    const uint32_t tx = (p->width + kTile - 1) / kTile, ty = (p->height + kTile - 1) / kTile;
+    const uint32_t tw = p->tile_w ? (uint32_t)p->tile_w : kTile, th = p->tile_h ? (uint32_t)p->tile_h : kTile;
+    const uint32_t tx = (p->width + tw - 1) / tw, ty = (p->height + th - 1) / th;
     const uint32_t ntiles = tx * ty;
     a.tiles_x = tx;
+    a.tile_w = tw; a.tile_h = th;
+    a.tile_bx = tw / kTile; a.tile_blocks = (tw / kTile) * (th / kTile);
+    a.morton_out = (p->pixel_order == PT_ORDER_MORTON) ? 1u : 0u;
     a.ntiles_shard = (ntiles > (uint32_t)p->shard_index) ? (ntiles - (uint32_t)p->shard_index + (uint32_t)p->shard_count - 1) / (uint32_t)p->shard_count : 0;
     a.cull_rel = 1.0f + 1.0f / 1024.0f;
     a.cull_abs = c->scene_extent * 1e-4f;
@@ -2296,7 +2339,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
 
     a.pixel_counter = c->pixel_counter;
-    a.nunits = a.ntiles_shard * 64u;
+    a.nunits = a.ntiles_shard * tw * th;
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
     a.root_first = c->wf_root_first;
@@ -2324,11 +2367,13 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
     const uint32_t waves_per_cu = 16;
     uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
-    if (grid > a.ntiles_shard) grid = a.ntiles_shard > 0 ? a.ntiles_shard : 1;
+    if (grid > a.ntiles_shard * a.tile_blocks) grid = a.ntiles_shard > 0 ? a.ntiles_shard * a.tile_blocks : 1;
     // the tile kernel traces with the render-path BVH4 walk under the wavefront kernel's conditions
     // (PT_TILE_FAST4=0: the reference-BVH culled walk, as before)
     a.tile_fast4 = (!refwalk && !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam && c->tile_fast4 && c->num_tris > 0) ? 1u : 0u;
     HIP_TRY(hipEventRecord(c->ev0, stream));
+    bool kernel_events = false;   // ek0/ek1 recorded around the integration kernel (wavefront path)
+    uint64_t units = 0, split = 0;
     if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
         // 4 waves per block; per wave an LDS ring of kRing packed entries x 64 lanes, deeper
         // entries spill to HBM (a BVH4 walk pushes at most 3 entries per level)
@@ -2344,7 +2389,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`
         // pixel slots are split into sample chunks, so the final units are short.
         // A shard with too few pixels to keep every resident lane busy is split entirely.
-        b.npix = a.ntiles_shard * 64u;
+        b.npix = a.ntiles_shard * tw * th;
         const uint32_t paths_per_block = 256u;
         const uint64_t lanes = (uint64_t)blocks * paths_per_block;   // concurrently running paths
         uint32_t chunks = 1, ntail = 0, nmid = 0, chunks_mid = 1;
@@ -2387,7 +2432,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         if (ntail > 0 && chunks > 1) {
             uint64_t budget;
             if (const char* e = getenv("PT_LBUF_BUDGET_MB")) {
-                budget = (uint64_t)std::max(0.0, atof(e)) * (1ull << 20);
+                budget = (uint64_t)(std::max(0.0, atof(e)) * (double)(1ull << 20));   // (fractional MB kept)
             } else {
                 size_t fr = 0, tot = 0;
                 HIP_TRY(hipMemGetInfo(&fr, &tot));
@@ -2471,22 +2516,36 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         }
         if (c->use_jump_bytes) {
             if (!c->jump_bytes) {   // once per context: 512 byte-sliced 160x160 GF(2) matrices (84 MB)
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->jump_bytes), (size_t)512 * 20 * 256 * kJumpEntryWords * 4));
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->seed_states), (size_t)256 * kJumpEntryWords * 4));
-                hipLaunchKernelGGL(build_jump_byte_tables, dim3(512 * 20), dim3(256), 0, stream, c->jump, c->jump_bytes);
-                HIP_TRY(hipGetLastError());
+                // (built into locals and published only once the build launched: a failure leaves the
+                // context without tables, so the next render tries again instead of seeding from garbage)
+                uint32_t *jb = nullptr, *ss = nullptr;
+                const bool ok = hipMalloc(reinterpret_cast<void**>(&jb), (size_t)512 * 20 * 256 * kJumpEntryWords * 4) == hipSuccess &&
+                                hipMalloc(reinterpret_cast<void**>(&ss), (size_t)256 * kJumpEntryWords * 4) == hipSuccess;
+                if (ok) hipLaunchKernelGGL(build_jump_byte_tables, dim3(512 * 20), dim3(256), 0, stream, c->jump, jb);
+                if (!ok || hipGetLastError() != hipSuccess) {
+                    if (jb) (void)hipFree(jb);
+                    if (ss) (void)hipFree(ss);
+                    return pt::fail(ok ? PT_E_HIP : PT_E_OOM, "pt_render: jump-table setup failed");
+                }
+                c->jump_bytes = jb;
+                c->seed_states = ss;
             }
             hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, c->seed_states);
             b.jump_bytes = c->jump_bytes;
             b.seed_states = c->seed_states;
         }
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
+        HIP_TRY(hipEventRecord(c->ek0, stream));
+        kernel_events = true;
+        units = b.nunits;
+        split = b.ntail;
         if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ek1, stream));
         if (b.ntail > 0) hipLaunchKernelGGL(finalize_pixels, dim3((b.ntail + 255) / 256), dim3(256), 0, stream, b);
         HIP_TRY(hipGetLastError());
         if (d_times) {
@@ -2538,11 +2597,15 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             }
         }
     }
-    float ms = 0.0f;
+    float ms = 0.0f, kms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (kernel_events) HIP_TRY(hipEventElapsedTime(&kms, c->ek0, c->ek1));
+    else kms = ms;   // (the tile kernel is the render's only launch)
     if (st) {
         st->seconds = ms * 1e-3;
-        st->kernel_ms = ms;
+        st->kernel_ms = kms;
+        st->work_units = units;
+        st->split_pixels = split;
         st->rays_traced = cnt[0];
         st->rays_reference = cnt[1];
         st->node_tests = cnt[2];
@@ -2562,6 +2625,51 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     return PT_OK;
 }
 
+}  // extern "C"
+
+int pt::copy_to_host(void* dst, const void* src, size_t bytes, void* stream_v, void** pinned, size_t* pinned_bytes)
+{
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+    if (*pinned_bytes < bytes) {
+        free_pinned(*pinned);
+        *pinned = nullptr;
+        *pinned_bytes = 0;
+        if (hipHostMalloc(pinned, bytes, hipHostMallocDefault) != hipSuccess) {
+            *pinned = nullptr;   // (no pinned memory: the runtime's own pageable path)
+            HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            return PT_OK;
+        }
+        *pinned_bytes = bytes;
+    }
+    HIP_TRY(hipMemcpyAsync(*pinned, src, bytes, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const unsigned nt = (unsigned)std::min<size_t>(pt::host_threads(), std::max<size_t>(1, bytes >> 21));   // >= 2 MB each
+    const char* s = static_cast<const char*>(*pinned);
+    char* d = static_cast<char*>(dst);
+    auto part = [&](unsigned k) {
+        const size_t b0 = (bytes * k / nt) & ~(size_t)4095, b1 = (k + 1 == nt) ? bytes : ((bytes * (k + 1) / nt) & ~(size_t)4095);
+        memcpy(d + b0, s + b0, b1 - b0);
+    };
+    if (nt <= 1) {
+        memcpy(d, s, bytes);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(nt - 1);
+        for (unsigned k = 1; k < nt; ++k) th.emplace_back(part, k);
+        part(0);
+        for (std::thread& t : th) t.join();
+    }
+    return PT_OK;
+}
+
+void pt::free_pinned(void* p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
+extern "C" {
+
 int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rgb, pt_stats* st)
 {
     if (!c || !p || !out_rgb) return pt::fail(PT_E_INVALID, "pt_render: null argument");
@@ -2575,11 +2683,10 @@ int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rg
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->scratch_out), bytes));
         c->scratch_bytes = bytes;
     }
-    HIP_TRY(hipMemset(c->scratch_out, 0, bytes));
+    HIP_TRY(hipMemsetAsync(c->scratch_out, 0, bytes, nullptr));
     int rc = pt_render_device(c, p, cam, c->scratch_out, nullptr, st);
     if (rc != PT_OK) return rc;
-    HIP_TRY(hipMemcpy(out_rgb, c->scratch_out, bytes, hipMemcpyDeviceToHost));
-    return PT_OK;
+    return pt::copy_to_host(out_rgb, c->scratch_out, bytes, nullptr, &c->pinned, &c->pinned_bytes);
 }
 
 }  // extern "C"
@@ -2654,6 +2761,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
     float* d_rays = nullptr;
     int32_t* d_tri = nullptr;
     float* d_t = nullptr;
+    uint32_t* d_cnt = nullptr;
     int rc = PT_OK;
     auto run = [&]() -> int {
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_rays), (size_t)n * 24));
@@ -2662,9 +2770,10 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
         HIP_TRY(hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
         HIP_TRY(hipMemset(c->counters, 0, kCounterWords * sizeof(unsigned long long)));
         const bool count = tri_counts != nullptr || spill_entries != nullptr;
-        if (tri_counts && c->num_tris > 0) {
-            HIP_TRY(hipMemset(c->tri_counts, 0, (size_t)c->num_tris * 4));
-            a.tri_counts = c->tri_counts;
+        if (tri_counts && c->num_tris > 0) {   // (own scratch: the last render's counts stay for pt_tri_counts)
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_cnt), (size_t)c->num_tris * 4));
+            HIP_TRY(hipMemset(d_cnt, 0, (size_t)c->num_tris * 4));
+            a.tri_counts = d_cnt;
         }
         const bool ref = (flags & PT_FLAG_REFERENCE_BVH) != 0;
         if (ref && count) hipLaunchKernelGGL((trace_rays<true, true>), dim3(blocks), dim3(256), lds, 0, a, d_rays, n, d_tri, d_t);
@@ -2676,7 +2785,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
         HIP_TRY(hipMemcpy(t_out, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
         if (tri_counts && c->num_tris > 0) {   // added to the caller's counts (kernel.cu:133 accumulates)
             std::vector<uint32_t> h(c->num_tris);
-            HIP_TRY(hipMemcpy(h.data(), c->tri_counts, (size_t)c->num_tris * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(h.data(), d_cnt, (size_t)c->num_tris * 4, hipMemcpyDeviceToHost));
             for (uint32_t k = 0; k < c->num_tris; ++k) tri_counts[k] += h[k];
         }
         if (spill_entries) {
@@ -2690,7 +2799,40 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
     if (d_rays) (void)hipFree(d_rays);
     if (d_tri) (void)hipFree(d_tri);
     if (d_t) (void)hipFree(d_t);
+    if (d_cnt) (void)hipFree(d_cnt);
     return rc;
+}
+
+extern "C" int pt_shard_pixels(int w, int h, int shard_index, int shard_count, int tile_w, int tile_h, uint32_t* out,
+                               uint32_t cap, uint32_t* n_out)
+{
+    pt::clear_error();
+    if (w <= 0 || h <= 0 || w > 65535 || h > 65535 || shard_count < 1 || shard_index < 0 || shard_index >= shard_count || !n_out)
+        return pt::fail(PT_E_INVALID, "pt_shard_pixels: bad arguments");
+    for (const int v : {tile_w, tile_h})
+        if (v != 0 && (v < 8 || v > 256 || v % 8 != 0)) return pt::fail(PT_E_INVALID, "pt_shard_pixels: tile size %dx%d", tile_w, tile_h);
+    TileMap m;
+    m.w = w; m.h = h; m.shard_index = shard_index; m.shard_count = shard_count;
+    m.tile_w = tile_w ? (uint32_t)tile_w : kTile;
+    m.tile_h = tile_h ? (uint32_t)tile_h : kTile;
+    m.tiles_x = ((uint32_t)w + m.tile_w - 1) / m.tile_w;
+    const uint32_t ntiles = m.tiles_x * (((uint32_t)h + m.tile_h - 1) / m.tile_h);
+    m.tile_bx = m.tile_w / kTile;
+    m.tile_blocks = m.tile_bx * (m.tile_h / kTile);
+    const uint32_t nts = (ntiles > (uint32_t)shard_index) ? (ntiles - (uint32_t)shard_index + (uint32_t)shard_count - 1) / (uint32_t)shard_count : 0u;
+    const uint64_t slots = (uint64_t)nts * m.tile_w * m.tile_h;
+    uint32_t n = 0;
+    for (uint64_t q = 0; q < slots; ++q) {
+        uint32_t px, py;
+        if (!unit_pixel(m, (uint32_t)q, &px, &py)) continue;
+        if (out) {
+            if (n >= cap) return pt::fail(PT_E_INVALID, "pt_shard_pixels: buffer of %u entries too small", cap);
+            out[n] = py * (uint32_t)w + px;
+        }
+        ++n;
+    }
+    *n_out = n;
+    return PT_OK;
 }
 
 extern "C" int pt_tonemap_device(pt_ctx* c, const float* d_rgb, int w, int h, int32_t* d_codes, void* stream_v)

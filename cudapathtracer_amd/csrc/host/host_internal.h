@@ -72,6 +72,13 @@ bool tonemap_thresholds(float t[256]);
 // host threads for the parallel builders: PT_HOST_THREADS, else OMP_NUM_THREADS, else the
 // hardware concurrency, capped at 16
 unsigned host_threads();
+bool morton_size_ok(int w, int h);   // square power-of-two image (the reference's Morton imgBuff)
+// Device -> host copy of a finished image through a pinned staging buffer (*pinned, grown as needed,
+// owned by the caller's context / group; freed with free_pinned): one DMA on `stream` (a
+// hipStream_t), then host_threads() threads copy the staging buffer into dst -- a pageable
+// destination's first-touch page faults spread over the threads instead of serialising the DMA.
+int copy_to_host(void* dst, const void* src_dev, size_t bytes, void* stream, void** pinned, size_t* pinned_bytes);
+void free_pinned(void* pinned);
 
 // ---- render-path acceleration structure (accel_build.cpp) --------------------------------
 struct AccelNode {

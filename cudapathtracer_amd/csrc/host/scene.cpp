@@ -231,15 +231,20 @@ int pt_tonemap_u8(double c)
 
 namespace {
 template <typename T>
-int write_ppm_any(const char* path, const T* rgb, int w, int h)
+int write_ppm_any(const char* path, const T* rgb, int w, int h, int order = PT_ORDER_SCANLINE)
 {
     if (!path || !rgb || w <= 0 || h <= 0) return fail(PT_E_INVALID, "pt_write_ppm: bad arguments");
+    if (order != PT_ORDER_SCANLINE && order != PT_ORDER_MORTON) return fail(PT_E_INVALID, "pt_write_ppm: pixel order %d", order);
+    if (order == PT_ORDER_MORTON && !pt::morton_size_ok(w, h))
+        return fail(PT_E_INVALID, "pt_write_ppm: Morton order needs a square power-of-two image (%dx%d)", w, h);
     FILE* fp = fopen(path, "w");
     if (!fp) return fail(PT_E_IO, "pt_write_ppm: cannot open %s", path);
     fprintf(fp, "P3 %d %d 255\n", w, h);
     for (int y = 0; y < h; ++y) {
         for (int x = w - 1; x >= 0; --x) {                                     // mirrored, kernel.cu:766
-            const T* p = rgb + (static_cast<size_t>(y) * w + x) * 3;
+            const size_t idx = order == PT_ORDER_MORTON ? pt_morton_pxl_to_i((uint32_t)x, (uint32_t)y)   // kernel.cu:771
+                                                        : static_cast<size_t>(y) * w + x;
+            const T* p = rgb + idx * 3;
             fprintf(fp, "%d %d %d ", pt_tonemap_u8(static_cast<double>(p[0])), pt_tonemap_u8(static_cast<double>(p[1])),
                     pt_tonemap_u8(static_cast<double>(p[2])));
         }
@@ -252,6 +257,11 @@ int write_ppm_any(const char* path, const T* rgb, int w, int h)
 extern "C" int pt_write_ppm(const char* path, const float* rgb, int width, int height)
 {
     return write_ppm_any(path, rgb, width, height);
+}
+
+extern "C" int pt_write_ppm_order(const char* path, const float* rgb, int width, int height, int pixel_order)
+{
+    return write_ppm_any(path, rgb, width, height, pixel_order);
 }
 
 // The reference's PPM text (kernel.cu:763-778) from tone-mapped codes (pt_tonemap / GPU).
@@ -287,6 +297,13 @@ extern "C" int pt_write_pfm(const char* path, const float* rgb, int w, int h)
 }
 
 namespace pt {
+// the sizes for which the reference's Morton framebuffer (idx < W*H, camera.h:57-75) covers the
+// image one-to-one: square powers of two
+bool morton_size_ok(int w, int h)
+{
+    return w > 0 && w == h && (w & (w - 1)) == 0 && w <= 65536;
+}
+
 unsigned host_threads()
 {
     for (const char* var : {"PT_HOST_THREADS", "OMP_NUM_THREADS"}) {

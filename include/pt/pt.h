@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5
+#define PT_ABI_VERSION 6
 
 /* ---- status codes */
 #define PT_OK 0
@@ -123,6 +123,9 @@ void pt_camera_ray(const pt_camera* cam, uint32_t idx, int lens, float u1, float
  * pt_render (pixel (x,y) at rgb[(y*W + x)*3]); the f64 variant takes the reference's own
  * double accumulator type. */
 int pt_write_ppm(const char* path, const float* rgb, int width, int height);
+/* Same for a buffer in either pixel order (PT_ORDER_MORTON: the reference's imgBuffer_host
+ * indexing, kernel.cu:771; square power-of-two sizes only). */
+int pt_write_ppm_order(const char* path, const float* rgb, int width, int height, int pixel_order);
 int pt_write_ppm_f64(const char* path, const double* rgb, int width, int height);
 /* PPM tone map of one value: (int)(pow(c/(c+1), (double)(float)(1/2.2)) * 255). */
 int pt_tonemap_u8(double c);
@@ -158,12 +161,25 @@ typedef struct {
     uint32_t flags;          /* PT_FLAG_*                                                           */
     uint64_t seed;           /* curand_init seed (kernel.cu:532 uses 1234)                          */
     int32_t shard_index;     /* this renderer's shard in [0, shard_count)                           */
-    int32_t shard_count;     /* image tiles (8x8) are dealt round-robin: tile t -> shard t % count  */
+    int32_t shard_count;     /* image tiles (tile_w x tile_h) are dealt round-robin: tile t -> shard
+                                t % count, tiles numbered row-major                                 */
+    int32_t pixel_order;     /* PT_ORDER_*: how the output buffer is indexed                        */
+    int32_t tile_w, tile_h;  /* shard tile size in pixels: 0 = 8; multiples of 8 up to 256           */
 } pt_params;
 
+/* pt_params.pixel_order.  SCANLINE: pixel (x,y) at out[(y*W + x)*3 + k].  MORTON: at
+ * out[mortonPxltoI(x,y)*3 + k] -- the reference's own imgBuff indexing (drawPixel writes
+ * imgBuff[idx] with idx the Morton index, kernel.cu:543,552; the PPM loop reads
+ * imgBuffer_host[cam.mortonPxltoI(x,y)], kernel.cu:771), defined only where the reference's is:
+ * square power-of-two images (others: PT_E_INVALID). */
+#define PT_ORDER_SCANLINE 0
+#define PT_ORDER_MORTON 1
+
 typedef struct {
-    double seconds;            /* device time of the render kernels (hipEvent pair)              */
-    double kernel_ms;          /* same, in ms, of the dominant (integration) kernel               */
+    double seconds;            /* device time of the whole render (hipEvent pair around every
+                                  launch: RNG seeding, integration, split-pixel finalisation)     */
+    double kernel_ms;          /* device time of the integration kernel alone, in ms (its own
+                                  hipEvent pair)                                                  */
     uint64_t samples;          /* pixel samples computed                                         */
     uint64_t rays_traced;      /* trace() calls actually executed on the device                   */
     uint64_t rays_reference;   /* trace() calls the reference integrator performs for the same
@@ -189,6 +205,9 @@ typedef struct {
                                   fixed stack[64] of kernel.cu:114 has no such tier)              */
     uint64_t lds_node_tests;   /* PT_FLAG_COUNT, wavefront kernel: the node_tests served by the copy
                                   of the BVH4's top nodes in LDS (no vector-memory fetch)         */
+    uint64_t work_units;       /* wavefront kernel: work units of this render (whole pixels + sample
+                                  chunks of split pixels); 0 for the tile kernel                  */
+    uint64_t split_pixels;     /* wavefront kernel: pixel slots split into sample chunks          */
 } pt_stats;
 
 /* Host-only diagnostic: builds the render path's private acceleration structure for `scene`
@@ -200,8 +219,9 @@ int pt_accel_digest(const pt_scene* scene, uint64_t* digest, uint32_t* num_nodes
 /* Upload a scene to HIP device `device` (ordinal among visible devices). */
 pt_ctx* pt_create(const pt_scene* scene, int device, int* err);
 
-/* Render into a HOST buffer out_rgb[W*H*3] (fp32 mean radiance, scanline order).  Pixels
- * outside this shard are written as 0.  Blocking. */
+/* Render into a HOST buffer out_rgb[W*H*3] (fp32 mean radiance, in params->pixel_order).  Pixels
+ * outside this shard are written as 0.  Blocking.  The image leaves the device through a pinned
+ * staging buffer owned by the context (one DMA, then a parallel host copy into out_rgb). */
 int pt_render(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float* out_rgb, pt_stats* stats);
 
 /* Same into a DEVICE buffer d_out[W*H*3] on `stream` (a hipStream_t, NULL = default stream).
@@ -250,6 +270,13 @@ int pt_tonemap(pt_ctx* ctx, const float* rgb, int width, int height, int32_t* co
  * are summed over the shards; `seconds` is the job's wall time (renders + reduce + copy).
  * Replaces the reference's launch loop (kernel.cu:709-736) and its D2H copy (:760).
  * The group does not own the contexts; destroy it before them. */
+/* The pixels shard `shard_index` of `shard_count` renders (tile_w x tile_h tiles, 0 = 8, dealt tile t ->
+ * shard t % count): their scanline ids y*W + x, in the order the shard's work slots take them (8x8
+ * blocks, Morton order within a block).  out = NULL: only *n_out.  Host-only; the kernels use the same
+ * mapping function. */
+int pt_shard_pixels(int width, int height, int shard_index, int shard_count, int tile_w, int tile_h, uint32_t* out,
+                    uint32_t cap, uint32_t* n_out);
+
 typedef struct pt_group pt_group;
 pt_group* pt_group_create(pt_ctx* const* ctxs, int n, int* err);
 int pt_group_size(const pt_group* group);

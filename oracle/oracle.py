@@ -89,6 +89,8 @@ def lib():
         h.or_render.argtypes = [C.POINTER(OScene), C.POINTER(OCamera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                 C.c_uint64, C.c_void_p, C.c_uint32, C.c_int, C.c_void_p, C.POINTER(OCounters)]
         h.or_render.restype = C.c_int
+        h.or_write_ppm_imgbuf.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
+        h.or_write_ppm_imgbuf.restype = C.c_int
         _lib = h
     return _lib
 
@@ -190,3 +192,23 @@ def jump_images(log2_steps):
 
 def refgen_available():
     return os.path.exists(REFGEN)
+
+
+def write_ppm_imgbuf(path, imgbuf, width, height):
+    """kernel.cu:763-778 restated: the reference's PPM loop over a Morton-indexed (W*H, 3) buffer
+    (its imgBuffer_host, f64; an fp32 buffer is widened exactly)."""
+    buf = np.ascontiguousarray(imgbuf, dtype=np.float64).reshape(-1)
+    assert buf.size == width * height * 3
+    if lib().or_write_ppm_imgbuf(str(path).encode(), buf.ctypes.data, int(width), int(height)) != 0:
+        raise OSError("or_write_ppm_imgbuf: cannot write %s" % path)
+
+
+def ref_ppm_imgbuf(imgbuf, width, height, workdir):
+    """The reference's OWN loop (refgen ppm: kernel.cu:763-778 compiled verbatim) on the same buffer;
+    returns the PPM bytes.  Build container only (needs oracle/_ref/refgen)."""
+    buf = np.ascontiguousarray(imgbuf, dtype=np.float64).reshape(-1)
+    inp = os.path.join(workdir, "imgbuf.bin")
+    buf.tofile(inp)
+    subprocess.check_call([REFGEN, "ppm", inp, str(width), str(height)], cwd=workdir)
+    with open(os.path.join(workdir, "image.ppm"), "rb") as fh:
+        return fh.read()

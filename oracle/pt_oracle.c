@@ -12,6 +12,7 @@
 #include "pt_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -681,4 +682,28 @@ int or_render(const or_scene* sc, const or_camera* cam, int width, int height,
     }
     if (cnt) { cnt->traces += tr; cnt->node_tests += nt; cnt->tri_tests += tt; }
     return 0;
+}
+
+/* kernel.cu:763-778 (the reference's "save the file" loop) over its Morton-indexed imgBuffer_host;
+ * color.h:59-62 normalized = c/(c+1) per channel, color.h:68-71 gammaCorrect = pow(c, (float)(1/2.2))
+ * (the exponent is a float parameter), then (int)(c*255) */
+static int tone_ref(double c)
+{
+    const double n = c / (c + 1);
+    const double g = pow(n, (double)(float)(1 / 2.2));
+    return (int)(g * 255);
+}
+
+int or_write_ppm_imgbuf(const char* path, const double* imgbuf, int width, int height)
+{
+    FILE* fp = fopen(path, "w");
+    if (!fp) return -1;
+    fprintf(fp, "P3 %d %d 255\n", width, height);
+    for (int y = 0; y < height; ++y) {
+        for (int x = width - 1; x >= 0; --x) {
+            const double* c = imgbuf + (size_t)or_morton_pxl_to_i((uint32_t)x, (uint32_t)y) * 3;   /* :771 */
+            fprintf(fp, "%d %d %d ", tone_ref(c[0]), tone_ref(c[1]), tone_ref(c[2]));
+        }
+    }
+    return fclose(fp) == 0 ? 0 : -1;
 }

@@ -112,6 +112,12 @@ int      or_render(const or_scene* sc, const or_camera* cam, int width, int heig
                    const uint32_t* pixels, uint32_t num_pixels, int threads,
                    double* out, or_counters* cnt);
 
+/* ---- output (kernel.cu:763-778, color.h:59-71): the reference's PPM loop over its Morton-indexed
+ * framebuffer imgBuffer_host (W*H x 3 f64, pixel (x,y) at mortonPxltoI(x,y)): "P3 W H 255\n", rows
+ * y ascending, x descending, "%d %d %d " of (int)(gammaCorrect(normalized(c), 1/2.2)*255).
+ * Returns 0, or -1 when the file cannot be written. */
+int      or_write_ppm_imgbuf(const char* path, const double* imgbuf, int width, int height);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,11 @@
 //                scene's buildBVH() array; counts: numTris x u32, the trace()'s test[] increments summed
 //                over all rays (kernel.cu:133; sized numTris here -- the reference's buffer has
 //                bvh.size = numTris-1 entries, kernel.cu:696, so its last increment lands out of bounds)
+//   refgen ppm   <imgbuf.bin> <W> <H>  (writes ./image.ppm, as the reference does)
+//                in: W*H x 3 f64, the reference's imgBuffer_host (Morton-indexed: kernel.cu:543,552); the
+//                PPM is written by the reference's own output loop (kernel.cu:763-778, "save the file"),
+//                extracted verbatim into oracle/_ref/ref_ppm.inc by oracle/Makefile, with IMAGE_WIDTH /
+//                IMAGE_HEIGHT (kernel.cu:28-29 #defines) bound to W and H
 #include <cstdint>
 #include <cmath>
 #include <cstdio>
@@ -207,6 +212,26 @@ int main(int argc, char** argv)
         }
         spit(argv[3], out.data(), out.size());
         spit(argv[4], test.data(), test.size() * 4);
+        return 0;
+    }
+#endif
+#ifdef REFGEN_PPM
+    if (cmd == "ppm") {
+        std::vector<char> in = slurp(argv[2]);
+        const int img_w = atoi(argv[3]), img_h = atoi(argv[4]);
+        if ((size_t)img_w * (size_t)img_h * 24 != in.size()) { fprintf(stderr, "refgen ppm: size mismatch\n"); return 2; }
+        const double* p = (const double*)in.data();
+        std::vector<color> imgBuffer_host_v((size_t)img_w * img_h);
+        for (size_t i = 0; i < imgBuffer_host_v.size(); ++i)
+            imgBuffer_host_v[i] = color(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+        color* imgBuffer_host = imgBuffer_host_v.data();
+        camera cam;   // (only mortonPxltoI is used, which reads no field)
+        memset(&cam, 0, sizeof(cam));
+#define IMAGE_WIDTH img_w
+#define IMAGE_HEIGHT img_h
+#include REFGEN_PPM   // kernel.cu:763-778, verbatim
+#undef IMAGE_WIDTH
+#undef IMAGE_HEIGHT
         return 0;
     }
 #endif

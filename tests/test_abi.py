@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_error_channel():
     L = _lib.lib()
-    assert L.pt_abi_version() == 5
+    assert L.pt_abi_version() == 6
     rc = L.pt_render(None, None, None, None, None)
     assert rc == _lib.PT_E_INVALID
     assert b"null" in L.pt_last_error()

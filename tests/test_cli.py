@@ -82,3 +82,25 @@ def test_cli_tri_counts_csv_matches_reference_walk(tmp_path):
     oracle.render(osc, oracle.camera((0.0, 1.0, 3.0), 1.0, 3.0, 0.0, w, h), w, h, spp, 3, 0, 1234, tri_counts=counts)
     assert len(got) == len(counts) - 1
     assert np.array_equal(got, counts[:-1])
+
+
+@pytest.mark.gpu
+def test_cli_morton_and_multi_gpu_match_one_gpu(tmp_path):
+    """--morton renders into the reference's Morton imgBuff and writes the PPM through the Morton map
+    (kernel.cu:771): same bytes as the scanline run.  --gpus 2 (pt_render_multi: tile shards + RCCL
+    reduce) runs only where two devices are visible, and must write the same bytes."""
+    import torch
+    base = _obj_args("cornell_blob") + ["--width", "32", "--height", "32", "--spp", "3", "--quiet"]
+    a, b = str(tmp_path / "a.ppm"), str(tmp_path / "b.ppm")
+    pa, pb = str(tmp_path / "a.pfm"), str(tmp_path / "b.pfm")
+    r = _run(base + ["--out", a, "--pfm", pa])
+    assert r.returncode == 0, r.stderr
+    r = _run(base + ["--out", b, "--pfm", pb, "--morton", "--tile", "16x16"])
+    assert r.returncode == 0, r.stderr
+    assert open(a, "rb").read() == open(b, "rb").read()
+    assert open(pa, "rb").read() == open(pb, "rb").read()
+    if torch.cuda.device_count() >= 2:
+        c = str(tmp_path / "c.ppm")
+        r = _run(base + ["--out", c, "--gpus", "2"])
+        assert r.returncode == 0, r.stderr
+        assert open(a, "rb").read() == open(c, "rb").read()

@@ -305,14 +305,23 @@ def test_per_triangle_counts_match_reference(oracle_mod, cb, integ):
 @pytest.mark.parametrize("budget", ["0", "0.002"])
 def test_split_buffer_budget_fallback_bit_exact(oracle_mod, monkeypatch, budget):
     """Split pixels keep per-sample radiance (24 B per sample); over the memory budget
-    (PT_LBUF_BUDGET_MB) the split shrinks -- to nothing at 0, to a few slots at 2 KB -- and the
-    shards still sum to the oracle's image bit for bit."""
-    monkeypatch.setenv("PT_LBUF_BUDGET_MB", budget)
+    (PT_LBUF_BUDGET_MB) the split shrinks -- to nothing at 0, to a few slots at 2 KB (the partial
+    cap: 14 slots of 144 B, the rest whole-pixel units) -- and the shards still sum to the oracle's
+    image bit for bit."""
     s = load_scene("cornell_blob")
     w, h, spp = 64, 48, 6
     cam = pt.make_camera(width=w, height=h, **CAM)
     with pt.Renderer(s, 0) as r:
+        _, st0 = r.render(cam, w, h, spp, bounces=3)   # (no budget set: every pixel of this small image split)
+    assert st0["split_pixels"] == w * h
+    monkeypatch.setenv("PT_LBUF_BUDGET_MB", budget)
+    with pt.Renderer(s, 0) as r:
         full, st = r.render(cam, w, h, spp, bounces=3)
+        if budget == "0":
+            assert st["split_pixels"] == 0 and st["work_units"] == w * h
+        else:
+            assert st["split_pixels"] == (2097 // (spp * 24))
+            assert w * h < st["work_units"] < st0["work_units"]
         parts = np.zeros_like(full)
         for k in range(4):
             part, _ = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=4)
@@ -342,3 +351,80 @@ def test_group_render_one_device_equals_render(cb):
         with pytest.raises(pt.PtError) as e:
             pt.Group([r, r2])
         assert e.value.code == pt.PT_E_INVALID
+
+
+@pytest.mark.parametrize("integ", [0, 1])
+def test_morton_pixel_order_and_tile_sizes(oracle_mod, cb, tmp_path, integ):
+    """pt_params.pixel_order = PT_ORDER_MORTON writes pixel (x,y) at out[mortonPxltoI(x,y)] -- the
+    reference's imgBuff (kernel.cu:543,552) -- so the reference's own PPM loop (kernel.cu:763-778,
+    restated by the oracle and pinned to the compiled loop by kat_ppm_morton.npz) turns the buffer into
+    the bytes pt_write_ppm makes from the scanline render.  tile_w/tile_h change only which shard renders
+    a pixel: shards of 16x24 and 32x8 tiles sum to the same bits, in either order."""
+    s, r = cb
+    w = h = 64
+    spp = 3
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    scan, st = r.render(cam, w, h, spp, bounces=3, integrator=integ)
+    mort, stm = r.render(cam, w, h, spp, bounces=3, integrator=integ, pixel_order=pt.PT_ORDER_MORTON)
+    assert mort.shape == (w * h, 3)
+    assert np.array_equal(shard.to_scanline(mort, w, h).view(np.uint32), scan.view(np.uint32))
+    ref, _ = _oracle(oracle_mod, s, w, h, spp, 3, integ)
+    assert _bits_equal(scan, ref) == 0
+    a, b, c = str(tmp_path / "a.ppm"), str(tmp_path / "b.ppm"), str(tmp_path / "c.ppm")
+    pt.write_ppm(a, scan)
+    oracle_mod.write_ppm_imgbuf(b, mort, w, h)                       # the reference's loop, unchanged
+    pt.write_ppm(c, mort, pixel_order=pt.PT_ORDER_MORTON, width=w, height=h)
+    assert open(a, "rb").read() == open(b, "rb").read() == open(c, "rb").read()
+    for tw, th, n in ((16, 24, 3), (32, 8, 2), (64, 64, 5)):
+        for order, full in ((pt.PT_ORDER_SCANLINE, scan), (pt.PT_ORDER_MORTON, mort)):
+            acc = np.zeros_like(full)
+            for k in range(n):
+                part, _ = r.render(cam, w, h, spp, bounces=3, integrator=integ, shard_index=k, shard_count=n,
+                                   pixel_order=order, tile_w=tw, tile_h=th)
+                pix = shard.shard_pixels(w, h, k, n, tw, th)
+                if order == pt.PT_ORDER_MORTON:
+                    pix = shard.morton_index(pix % w, pix // w).astype(np.int64)
+                mask = np.zeros(w * h, dtype=bool)
+                mask[pix] = True
+                assert np.all(part.reshape(-1, 3)[~mask] == 0)
+                acc += part
+            assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+    # the reference's Morton buffer is defined for square power-of-two images only
+    for bw, bh in ((64, 32), (48, 48)):
+        with pytest.raises(pt.PtError) as e:
+            r.render(pt.make_camera(width=bw, height=bh, **CAM), bw, bh, 1, pixel_order=pt.PT_ORDER_MORTON)
+        assert e.value.code == pt.PT_E_INVALID
+    with pytest.raises(pt.PtError):
+        r.render(cam, w, h, 1, tile_w=12, tile_h=8)
+
+
+def _devices():
+    import torch
+    return torch.cuda.device_count()
+
+
+def test_group_render_multi_device_equals_render():
+    """pt_render_group on every visible device (>= 2; skipped on a one-GPU box): shards rendered
+    concurrently, one ncclReduce over xGMI -- bit-identical to one device, also on a second frame that
+    reuses the group's buffers."""
+    n = _devices()
+    if n < 2:
+        pytest.skip("one visible device")
+    s = load_scene("cornell_blob")
+    w, h, spp = 64, 48, 4
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    rs = [pt.Renderer(s, d) for d in range(n)]
+    try:
+        ref, st = rs[0].render(cam, w, h, spp, bounces=3)
+        with pt.Group(rs) as g:
+            for _ in range(2):
+                img, gst = g.render(cam, w, h, spp, bounces=3)
+                assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+                assert gst["samples"] == st["samples"]
+            cam64 = pt.make_camera(width=64, height=64, **CAM)
+            mort, _ = g.render(cam64, 64, 64, spp, bounces=3, pixel_order=pt.PT_ORDER_MORTON)
+            scan, _ = rs[0].render(cam64, 64, 64, spp, bounces=3)
+            assert np.array_equal(shard.to_scanline(mort, 64, 64).view(np.uint32), scan.view(np.uint32))
+    finally:
+        for r in rs:
+            r.close()

@@ -141,6 +141,44 @@ def test_tonemap_and_ppm_match_reference(tmp_path):
     assert os.path.getsize(str(tmp_path / "y.ppm")) > 0
 
 
+def test_morton_framebuffer_ppm_matches_reference_loop(tmp_path):
+    """The reference's framebuffer is Morton-indexed (drawPixel writes imgBuff[idx], kernel.cu:543,552)
+    and its PPM loop reads imgBuffer_host[cam.mortonPxltoI(x,y)] (kernel.cu:771).  Fixture: that loop
+    compiled verbatim from kernel.cu:763-778 (refgen ppm) over a 64x64 Morton buffer.  Byte-identical:
+    pt_write_ppm_order(MORTON) on the buffer, pt_write_ppm on its scanline reordering, and the
+    oracle's restatement of the loop."""
+    import oracle
+    from cudapathtracer_amd import shard
+    g = golden("kat_ppm_morton.npz")
+    buf, w, h, ref = g["buf"], int(g["w"]), int(g["h"]), g["ppm"].tobytes()
+    pm, ps, po = str(tmp_path / "m.ppm"), str(tmp_path / "s.ppm"), str(tmp_path / "o.ppm")
+    pt.write_ppm(pm, buf, pixel_order=pt.PT_ORDER_MORTON, width=w, height=h)
+    pt.write_ppm(ps, shard.to_scanline(buf, w, h))
+    oracle.write_ppm_imgbuf(po, buf, w, h)
+    for p in (pm, ps, po):
+        assert open(p, "rb").read() == ref, p
+    if oracle.refgen_available():   # build container: the reference's loop, live
+        assert oracle.ref_ppm_imgbuf(buf, w, h, str(tmp_path)) == ref
+    # the reference's Morton buffer covers the image only for square power-of-two sizes
+    for bw, bh in ((64, 32), (48, 48), (3, 3)):
+        with pytest.raises(pt.PtError) as e:
+            pt.write_ppm(str(tmp_path / "bad.ppm"), np.zeros((bw * bh, 3), np.float32), pixel_order=pt.PT_ORDER_MORTON,
+                         width=bw, height=bh)
+        assert e.value.code == pt.PT_E_INVALID
+
+
+def test_shard_tiles_partition_the_image():
+    """Tile shards (tile t -> shard t % N, tile_w x tile_h tiles of 8x8 blocks) partition every image."""
+    from cudapathtracer_amd import shard
+    for w, h in ((64, 64), (100, 77), (1, 1), (8, 200)):
+        for tw, th in ((0, 0), (16, 24), (32, 8), (256, 256)):
+            for n in (1, 3, 8):
+                allp = np.concatenate([shard.shard_pixels(w, h, k, n, tw, th) for k in range(n)])
+                assert len(allp) == w * h and len(np.unique(allp)) == w * h
+    with pytest.raises(ValueError):
+        shard.tiles_shape(64, 64, 12, 8)
+
+
 def test_structs_match_reference_layouts():
     assert api.VEC3.itemsize == 12 and api.TRI.itemsize == 28 and api.MAT.itemsize == 48 and api.NODE.itemsize == 32
 

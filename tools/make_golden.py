@@ -19,7 +19,11 @@ Outputs (all small, committed):
                                      tests/raysets.py: (triIndex, t) per ray + per-triangle test[]
                                      counts (kernel.cu:133) summed over the rays
 
-`python tools/make_golden.py --only trace` regenerates only the kat_trace_* files.
+  kat_ppm_morton.npz                 the reference's own PPM loop (kernel.cu:763-778, compiled verbatim:
+                                     refgen ppm) over a Morton-indexed imgBuffer_host (64x64 f32 values
+                                     incl. 0, huge, inf, NaN): the input buffer and the PPM bytes
+
+`python tools/make_golden.py --only trace|ppm` regenerates only the kat_trace_* / kat_ppm_* files.
 """
 from __future__ import annotations
 
@@ -257,12 +261,31 @@ def kat_trace(tmp):
         print("kat_trace", name, len(rays), "rays,", int((tri >= 0).sum()), "hits,", int(counts.sum()), "tests")
 
 
+def kat_ppm_morton(tmp):
+    """The reference's PPM loop (kernel.cu:763-778) over a Morton-indexed 64x64 imgBuffer_host."""
+    rng = np.random.default_rng(763)
+    w = h = 64
+    buf = (rng.random((w * h, 3)) * rng.choice([0.01, 1.0, 30.0], size=(w * h, 1))).astype(np.float32)
+    buf[:8] = [[0, 0, 0], [1e30, 3e38, np.inf], [np.nan, 1, 2], [1e-30, 0.5, 1e-7], [2.0, 0.25, 255.0],
+               [0.0123, 0.9, 7.5], [1.0, 1.0, 1.0], [100.0, 1000.0, 1e4]]
+    d = os.path.join(tmp, "ppm")
+    os.makedirs(d, exist_ok=True)
+    ppm = oracle.ref_ppm_imgbuf(buf, w, h, d)
+    np.savez_compressed(os.path.join(GOLD, "kat_ppm_morton.npz"), buf=buf, w=w, h=h,
+                        ppm=np.frombuffer(ppm, dtype=np.uint8))
+    print("kat_ppm_morton", len(ppm), "bytes")
+
+
 def main():
     if not os.path.exists(REFGEN):
         sys.exit("oracle/_ref/refgen missing: run `make -C oracle` with /root/reference present")
     if sys.argv[1:] == ["--only", "trace"]:
         with tempfile.TemporaryDirectory() as tmp:
             kat_trace(tmp)
+        return
+    if sys.argv[1:] == ["--only", "ppm"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            kat_ppm_morton(tmp)
         return
     os.makedirs(GOLD, exist_ok=True)
     if os.path.isdir(SCENES):
@@ -297,6 +320,7 @@ def main():
         kat_morton(tmp)
         kat_tone(tmp, rng)
         kat_trace(tmp)
+        kat_ppm_morton(tmp)
     xorwow_fixture()
     render_fixtures()
     print("golden fixtures written to", GOLD)

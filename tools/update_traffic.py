@@ -8,6 +8,7 @@ The file is stamped with the render kernel's source hash (bench.kernel_source_sh
 config, so bench.py uses it only for the kernel and workload it was measured on.
 
 usage: tools/update_traffic.py profiles/<tag> [W H SPP BOUNCES INTEGRATOR SHARDS]
+(entries of other configs are kept; the entry of this config is replaced)
 """
 import json
 import os
@@ -54,5 +55,13 @@ if "GRBM_GUI_ACTIVE" in c:
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
         b["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
     out["binding"] = b
-json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+# one entry per (config, source hash): a new measurement replaces the entry of its config
+path = os.path.join(ROOT, "profiles", "traffic.json")
+try:
+    tj = json.load(open(path))
+except (OSError, ValueError):
+    tj = {}
+entries = [e for e in tj.get("entries", []) if e.get("config") != cfg]
+entries.append(out)
+json.dump({"entries": entries}, open(path, "w"), indent=1)
 print(json.dumps(out, indent=1))
