@@ -257,7 +257,9 @@ def make_reduce(dist, backend, rank):
 
 
 def KERNEL_NAME(args):
-    return "render_unidir_wf" if not (args.flags & 1) else "render_tiles"
+    if args.flags & 1:   # PT_FLAG_REFERENCE_TRAVERSAL: the tile kernel
+        return "render_tiles"
+    return "render_head_wf" if args.integrator == 1 else "render_unidir_wf"
 
 
 def main():

@@ -518,6 +518,7 @@ struct W4 {
     float best_t;
     uint32_t best_slot;  // render-path triangle slot of the best hit, kNone = none
     uint32_t nx, ny, nz; // byte offsets in DNode4 of the near plane per axis (lo, or hi for inv < 0)
+    float occ;           // walk4_step<kAnyHit>: a hit with t <= occ ends the walk (any-hit); unused otherwise
 };
 
 // The exact reference test a winner must pass (DESIGN.md "Traversal" 2): the reference slab test
@@ -846,7 +847,9 @@ struct NoSetup {
 // kTop: the caller guarantees S.ntop >= 1 (no per-step test of an empty LDS top).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wsometimes-uninitialized"   // (a lane's triangle words, read only if it has a leaf)
-template <bool kCount, bool kTop = false, class Setup = NoSetup>
+// kAnyHit: the walk ends at the first hit with t <= w.occ (integrator 1's visibility rays: any such hit
+// decides "occluded"; the winner check still runs on it).
+template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
@@ -911,6 +914,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     }
     if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
     advance4(w, S, cull_rel, node_mask);
+    if (kAnyHit && w.best_t <= w.occ) return false;
     return w.node != kNone || leaf4_pending(w);
 }
 #pragma clang diagnostic pop

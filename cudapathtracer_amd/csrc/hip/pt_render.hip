@@ -106,6 +106,7 @@ struct Args {
     uint32_t num_emis;              // 0 = probe off
     unsigned long long* lane_times; // diagnostic (PT_LANE_TIMING): wall clock of each lane's end, then each
                                     // wave's start and exit (render_unidir_wf), or null
+    uint32_t head;                  // integrator 1 on the wavefront kernel (init_pixel_states' replay)
 };
 
 __device__ __forceinline__ V3 ld_norm(const DShade* s, int32_t tri)
@@ -798,6 +799,10 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     uint32_t done = 0;
     for (uint32_t c = 0; c < nc; ++c) {
         const uint32_t s0 = split ? chunk_first(a, c, nc) : 0u;
+        if (a.head) {   // integrator 1: a fixed 7 draws per sample (+2 lens): light pick 3, rand_ray 2, cosine 2
+            for (; done < s0; ++done)
+                for (int k = (lens ? 9 : 7); k > 0; --k) rng_next(r);
+        }
         for (; done < s0; ++done) replay_sample(r, lens, a.bounces);
         const size_t u = unit(c);
         st[u] = r.v0;
@@ -1397,8 +1402,574 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
     R.st4(CW_WGT + 4, dlo(wgt.b), dhi(wgt.b), rng.v4, nend);
 }
 
-template <bool kCount, int kMinWaves>
-__global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
+
+// The refill's unit dealing (as in shade_lane): lanes `idle` of the wave take the next units of this
+// shard from the unit counters; returns this lane's unit (`me`: this lane is idle), a.nunits once
+// every counter is exhausted.
+template <bool kCount>
+__device__ __forceinline__ uint32_t take_unit(const Args& a, int lane, uint64_t idle, bool me, const uint32_t* lprobe,
+                                              uint32_t* done_rel)
+{
+    uint32_t u = kNoUnit;
+    if (a.unit_queues > 1u) {
+        uint32_t qdone = *reinterpret_cast<volatile const uint32_t*>(lprobe + 1);
+        const uint32_t x0 = blockIdx.x & (kQueues - 1u);
+        for (uint32_t r = 0; r < kQueues && idle && qdone != (1u << kQueues) - 1u; ++r) {
+            const uint32_t x = (x0 + r) & (kQueues - 1u);
+            if (qdone & (1u << x)) continue;
+            const int leader = __ffsll((long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.pixel_counter + kQueueStride * (x + 1u), (uint32_t)__popcll(idle));
+            base = __shfl(base, leader, 64);
+            if (me && u == kNoUnit) {
+                const uint32_t k = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                const uint64_t uq = ((uint64_t)(k / kQueueBlock) * kQueues + x) * kQueueBlock + (k % kQueueBlock);
+                if (uq < a.nunits) u = (uint32_t)uq;
+            }
+            const uint64_t left = __ballot(me && u == kNoUnit);
+            if (left) {
+                qdone |= 1u << x;
+                if (lane == leader) atomicOr(const_cast<uint32_t*>(lprobe + 1), 1u << x);
+            }
+            idle = left;
+        }
+        if (me && u == kNoUnit) u = a.nunits;
+    } else {
+        const uint32_t need = (uint32_t)__popcll(idle);
+        const int leader = __ffsll((long long)idle) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(a.pixel_counter, need);
+        base = __shfl(base, leader, 64);
+        if (me) u = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+    }
+    if (kCount && me && u >= a.nunits) {   // queue drained; this lane's end after it and since the start
+        const unsigned long long now = wall_clock64();
+        atomicMin(a.counters + 21, now);
+        const unsigned long long d0 = __hip_atomic_load(a.counters + 21, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long s0 = __hip_atomic_load(a.counters + 20, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        done_rel[0] = (uint32_t)min(now - min(now, d0), 0xffffffffull);
+        done_rel[1] = (uint32_t)min(now - min(now, s0), 0xffffffffull);
+    }
+    return u;
+}
+// ------------------------------------------------------------------ wavefront kernel, integrator 1
+// radianceAlongSingleStep (kernel.cu:217-415) on the same state machine.  A sample is a fixed data
+// flow of traces: T1 the light subpath's bounce from the area-sampled light vertex x0 (kernel.cu:263-
+// 287), T2 the camera ray (the pixel's memo when the camera has no lens, :289-305), T3 the camera's
+// cosine bounce (:306-350), then one visibility ray x_i -> x_j for each connection (i in {0,1}, j in
+// {2,3}, :353-412) whose weight exceeds 0.01.  None of its XORWOW draws depends on a trace (lens 2,
+// light pick 3, rand_ray 2, cosine 2), so all of them are drawn when the sample starts.  The record
+// keeps the path vertices; the connection weights are recomputed from them in the sample's last pass,
+// in the reference's order, with the visibility bits the shadow walks left (the weights' arithmetic
+// is identical both times, so the set of connections that trace cannot differ).
+enum : int {
+    HW_N = 0, HW_STAGE, HW_FLAGS, HW_RNG_D,   // cell 0: sample, stage word, flags, XORWOW d
+    HW_RNG_V0 = 4,                            // cell 1: v0..v3
+    HW_RNG_V4 = 8, HW_NEND, HW_CU1, HW_CU2,   // cell 2: v4, unit end, the cosine draws (CU1: the pending
+                                              //         visibility ray's length once T3 has begun)
+    HW_X0 = 12, HW_MAT0 = 15,                 // cell 3: light vertex x0 (offset along its normal), material
+    HW_N0 = 16, HW_IP1 = 19,                  // cell 4: its normal, ip[1]
+    HW_X1 = 20, HW_MAT1 = 23,                 // cell 5: light bounce hit x1, material
+    HW_N1 = 24, HW_IP2 = 27,                  // cell 6: its normal, ip[2]
+    HW_X3 = 28, HW_MAT3 = 31,                 // cell 7: camera hit x3, material
+    HW_N3 = 32, HW_MAT2 = 35,                 // cell 8: its normal, material of x2
+    HW_X2 = 36, HW_G1 = 39,                   // cell 9: camera bounce hit x2, G of the light subpath edge x1-x0
+    HW_GC = 40,                               // cell 10: G of the four connections (written with T3's end)
+    HW_M = 44, HW_G3 = 50,                    // cells 11, 12.lo: running mean m0..m2 (f64); 12.z: G of x3-x2
+    HW_PXY = 52, HW_Q, HW_MTRI, HW_MT,        // cell 13: pixel (x | y << 16), split slot, primary memo (tri, t)
+    HW_CD = 56,                               // cell 14: camera direction (pinhole: the unit's; lens: the sample's)
+    HW_CO = 60,                               // cell 15: camera origin of a lens sample
+    kHeadWords = 64
+};
+// stage word: bits 0-1 the pending trace, 2-3 the connection whose visibility ray it is (k = 2i + j-2),
+// 4-7 visibility bits, 8-11 the connections that need a ray
+enum : uint32_t { HS_T1 = 0, HS_T2 = 1, HS_T3 = 2, HS_SH = 3 };
+constexpr int kHeadLdsLightBytes = (int)kLdsLights * 16;   // per staged light: its normal and material
+
+// The geometric factors of one HEAD sample's connections (kernel.cu:353-412): G1 = geo_term of the
+// light subpath edge x1-x0, G3 = of the camera edge x3-x2, Gc[k] = the connection term of (i, j),
+// k = 2i + j-2 -- the float parts of the weights, computed once from the vertices (x[4], nrm[4] as
+// radianceAlongSingleStep holds them); the f64 chain (head_weights) needs only these.
+struct HeadGeo {
+    float G1, G3, Gc[4];
+};
+__device__ __forceinline__ void head_geometry(const V3 (&x)[4], const V3 (&nrm)[4], HeadGeo& g)
+{
+    g.G1 = geo_term(x[1], x[0], nrm[1], nrm[0]);
+    g.G3 = geo_term(x[3], x[2], nrm[3], nrm[2]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 2; j < 4; ++j) {
+            const V3 seg = x[j] - x[i];
+            const V3 ray = normalized(seg);
+            float G = __builtin_fmaxf(0.0f, dot(ray, nrm[j]) * dot(ray * -1, nrm[i])) / dot(seg, seg);
+            if (G != G) G = 0;
+            g.Gc[2 * i + (j - 2)] = G;
+        }
+    }
+}
+// The four connections' weights in the reference's order and arithmetic: w = le*ip0, times
+// (albedo_k/pi, G, ip_k) for k = 1..i and k = j+1..3, times (albedo_j/pi, Gc, ip_j); a connection whose
+// weight max exceeds 0.01 traces (its bit in *need) and counts only if visible (bit in vis); the
+// radiance adds w*V and the camera hit's emission per connection.  mat[4] and ip[0..2] as the
+// reference's arrays (ip[3] = 1).
+__device__ __forceinline__ C3 head_weights(const Args& a, const int32_t (&mat)[4], const float (&ip)[3], const HeadGeo& g,
+                                           uint32_t vis, uint32_t* need)
+{
+    const C3 le = mat_emission(a.mats + mat[0]);
+    const C3 e3 = mat_emission(a.mats + mat[3]);
+    const C3 A1 = cdivf(mat_albedo(a.mats + mat[1]), 3.14159f);
+    const C3 A2 = cdivf(mat_albedo(a.mats + mat[2]), 3.14159f);
+    const C3 A3 = cdivf(mat_albedo(a.mats + mat[3]), 3.14159f);
+    C3 accum = c3(0, 0, 0);
+    uint32_t nd = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 2; j < 4; ++j) {
+            C3 w = cmulf(le, ip[0]);
+            if (i == 1) w = cmulf(cmulf(cmul(w, A1), g.G1), ip[1]);      // k = 1
+            if (j == 2) w = cmulf(cmulf(cmul(w, A3), g.G3), 1.0f);       // k = 3 (ip[3] = 1)
+            const int k = 2 * i + (j - 2);
+            w = cmulf(cmulf(cmul(w, (j == 2) ? A2 : A3), g.Gc[k]), (j == 2) ? ip[2] : 1.0f);
+            const float m = (float)fmax(w.r, fmax(w.g, w.b));
+            float V = 0;
+            if ((double)m > 0.01) {
+                nd |= 1u << k;
+                if (vis & (1u << k)) V = 1;
+            }
+            w = cmulf(w, V);
+            accum = cadd(accum, w);
+            accum = cadd(accum, e3);
+        }
+    }
+    if (need) *need = nd;
+    return accum;
+}
+
+__device__ __forceinline__ V3 u3f(uint4 q) { return v3(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z)); }
+
+// The visibility ray of connection k (kernel.cu:397-405: from x_i along normalized(x_j - x_i); visible
+// iff the hit's |t - len| <= 0.01) -- the expressions of head_connections, so the same bits.
+__device__ __forceinline__ void head_vis_ray(V3 xi, V3 xj, V3* ro, V3* rd, float* len)
+{
+    const V3 seg = xj - xi;
+    *len = length(seg);
+    *ro = xi;
+    *rd = normalized(seg);
+}
+// A visibility walk only needs hits up to len + 0.01: every t >= RN(len + 0.02) has |t - len| > 0.016
+// (len < MAX_FLOAT, so ulp(len) <= 2^-7), so the walk is bounded there and finding no hit below the
+// bound means "not visible" -- exactly as the reference's closest hit, wherever it lies beyond, does.
+__device__ __forceinline__ float head_vis_bound(float len)
+{
+    const float b = len + 0.02f;
+    return (b < kMaxFloat) ? b : kMaxFloat;
+}
+// ... and any hit with t <= RN(len - 0.03) decides "not visible" at once: then len - t >= 0.026 (exact, or
+// far larger), so |t - len| > 0.01 for it and for the closest hit, which is no farther (the walk stops
+// there; the winner check still confirms it is a triangle the reference tests).
+__device__ __forceinline__ float head_vis_occluded(float len)
+{
+    return (len > 0.04f) ? len - 0.03f : -1.0f;
+}
+
+template <bool kCount>
+__device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint32_t& state, V3& ro, V3& rd,
+                                                int32_t& htri, float& ht, W4& w, const Stack4& S,
+                                                unsigned long long* lcnt, const uint32_t* lprobe, uint32_t* done_rel,
+                                                Counters& cnt)
+{
+    const Args& a = kernel_args_opaque();
+    SEC(SEC_PASS);
+    const uint4 k0 = R.ld4(HW_N), k1 = R.ld4(HW_RNG_V0), k2 = R.ld4(HW_RNG_V4);
+    if (state == ST_CHECK) {
+        SEC(SEC_CHECK);
+        const float4 C = a.acc_tris[htri].c;
+        const float4 b0 = reinterpret_cast<const float4*>(a.wbox + htri)[0], b1 = reinterpret_cast<const float4*>(a.wbox + htri)[1];
+        htri = (int32_t)__float_as_uint(C.y);
+        state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
+    }
+    int n = (int)k0.x;
+    uint32_t stage = k0.y, fl = k0.z;
+    Rng rng;
+    rng.d = k0.w; rng.v0 = k1.x; rng.v1 = k1.y; rng.v2 = k1.z; rng.v3 = k1.w; rng.v4 = k2.x;
+    uint32_t nend = k2.y;
+    float cu1 = __uint_as_float(k2.z), cu2 = __uint_as_float(k2.w);
+    // (the staged light records and, behind them, each one's normal and material)
+    const DLight* const llt = reinterpret_cast<const DLight*>(lprobe + 4 + kMaxProbeEmitters * 12);
+    const float4* const lnm = reinterpret_cast<const float4*>(lprobe + 4 + kMaxProbeEmitters * 12 + kLdsLights * 12);
+
+    // begin a trace of (ro, rd) below `bound`; true = the lane continues shading at once (no triangles, a
+    // root miss -- the hit is a miss --, or a ray outside the Markstein preconditions: the exact slow walk)
+    auto begin_trace = [&](float bound, float occ) -> bool {
+        wave_count(lcnt + 0, lane);
+        SEC(SEC_BEGIN);
+        if (a.num_tris == 0) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }
+        if (!((a.scene_fast != 0u) && ray_fast(ro, rd))) { state = ST_SLOW; return true; }
+        if (!walk4_begin(w, ro, rd, a.acc_root, a.cull_abs)) { htri = -1; ht = kMaxFloat; state = ST_SHADE; return true; }
+        w.best_t = bound;
+        w.occ = occ;
+        state = ST_TRACE;
+        return false;
+    };
+    // a hit is at hand (after a walk, the slow walk or the memo): spheres, primary memo bookkeeping
+    auto take_hit = [&]() {
+        if (a.num_spheres && !(fl & CF_MEMO)) apply_spheres(a, ro, rd, &htri, &ht);
+        fl &= ~CF_MEMO;
+        if (fl & CF_PRIMARY) {
+            fl = (fl | CF_HAVE) & ~CF_PRIMARY;
+            R.st2(HW_MTRI, (uint32_t)htri, __float_as_uint(ht));
+            if (fl & CF_OWNER) {
+                const uint32_t q = R.ld(HW_Q);
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(a.pmemo) + q,
+                                   ((uint64_t)__float_as_uint(ht) << 32) | (uint32_t)(htri + 2), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                fl &= ~CF_OWNER;
+            }
+        }
+    };
+    // start sample n: all of its draws, the light vertex, the camera ray of a lens sample; trace T1
+    auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
+        SEC(SEC_START);
+        const bool lens = (fl & CF_LENS) != 0u;
+        float lu1 = 0.0f, lu2 = 0.0f;
+        if (lens) { lu1 = rng_uniform(rng); lu2 = rng_uniform(rng); }   // drawPixel's cameraRay (kernel.cu:547)
+        // light vertex: the area-CDF pick + uniform point (pick_light, kernel.cu:231-262)
+        float ra = a.total_light_area * rng_uniform(rng);
+        uint32_t sel = a.num_lights;
+        const bool staged = a.num_lights < kLdsLights;
+        const DLight* const lt = staged ? llt : a.lights;
+        for (uint32_t j = 0; j < a.num_lights && ra > 0; ++j) {
+            const float area = lt[j].area;
+            if (ra < area && ra > 0) sel = j;
+            ra -= area;
+        }
+        float u = rng_uniform(rng);
+        float v = rng_uniform(rng);
+        const DLight* L = lt + sel;
+        V3 p, n0;
+        int32_t m0;
+        if (L->pad != 0.0f) {   // sphere light (d8)
+            const float z = 1.0f - 2.0f * u;
+            const float rxy = sqrtf(__builtin_fmaxf(0.0f, 1.0f - z * z));
+            const float phi = (float)(2 * 3.14159 * (double)v);
+            float si, co;
+            det_sincos(phi, &si, &co);
+            p = v3(L->v0[0], L->v0[1], L->v0[2]) + v3(rxy * co, rxy * si, z) * L->a1[0];
+            n0 = prim_normal(a, L->tri, p);
+            m0 = prim_mat(a, L->tri);
+        } else {
+            if ((double)(u + v) > 1.0) {
+                u = (float)((double)u + 2 * (0.5 - (double)u));
+                v = (float)((double)v + 2 * (0.5 - (double)v));
+            }
+            p = v3(L->v0[0], L->v0[1], L->v0[2]) + v3(L->a1[0], L->a1[1], L->a1[2]) * u + v3(L->a2[0], L->a2[1], L->a2[2]) * v;
+            if (staged) {
+                const float4 q = lnm[sel];
+                n0 = v3(q.x, q.y, q.z);
+                m0 = (int32_t)__float_as_uint(q.w);
+            } else {
+                n0 = ld_norm(a.shade, L->tri);
+                m0 = ld_mat(a.shade, L->tri);
+            }
+        }
+        ro = p + n0 * 0.001f;                 // x[0] (kernel.cu:259)
+        rd = rand_ray(n0, rng);               // the light bounce (kernel.cu:264)
+        cu1 = rng_uniform(rng);               // cosine_ray's draws for T3 (kernel.cu:307)
+        cu2 = rng_uniform(rng);
+        R.st4(HW_X0, __float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), (uint32_t)m0);
+        R.st4(HW_N0, __float_as_uint(n0.x), __float_as_uint(n0.y), __float_as_uint(n0.z), 0u);
+        if (lens) {   // this sample's camera ray (its draws came first)
+            V3 co, cd;
+            camera_ray(a.cam, px, py, true, lu1, lu2, &co, &cd);
+            R.st4(HW_CD, __float_as_uint(cd.x), __float_as_uint(cd.y), __float_as_uint(cd.z), 0u);
+            R.st4(HW_CO, __float_as_uint(co.x), __float_as_uint(co.y), __float_as_uint(co.z), 0u);
+        }
+        stage = HS_T1;
+        wave_count(lcnt + 1, lane);
+        return begin_trace(kMaxFloat, -1.0f);
+    };
+    // T2: the camera ray -- the memo of a pinhole pixel, or a trace
+    auto camera_stage = [&]() -> bool {
+        stage = HS_T2;
+        wave_count(lcnt + 1, lane);
+        const uint4 cd = R.ld4(HW_CD);
+        rd = v3(__uint_as_float(cd.x), __uint_as_float(cd.y), __uint_as_float(cd.z));
+        const bool lens = (fl & CF_LENS) != 0u;
+        if (lens) {
+            const uint4 co = R.ld4(HW_CO);
+            ro = v3(__uint_as_float(co.x), __uint_as_float(co.y), __uint_as_float(co.z));
+        } else {
+            ro = v3(0.0f, 0.0f, 0.0f) + v3(fresh(a.cam.pos[0]), fresh(a.cam.pos[1]), fresh(a.cam.pos[2]));
+        }
+        if (fl & CF_HAVE) {
+            SEC(SEC_MEMO);
+            const uint2 mm = R.ld2(HW_MTRI);
+            htri = (int32_t)mm.x; ht = __uint_as_float(mm.y);
+            fl = (fl & ~CF_PRIMARY) | CF_MEMO; state = ST_SHADE;
+            return true;
+        }
+        if (fl & CF_SHARE) {
+            const uint32_t q = R.ld(HW_Q);
+            const uint64_t mv = __hip_atomic_load(reinterpret_cast<uint64_t*>(a.pmemo) + q, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)mv != 0u) {
+                htri = (int32_t)((uint32_t)mv - 2u);
+                ht = __uint_as_float((uint32_t)(mv >> 32));
+                fl = (fl | CF_PRIMARY | CF_MEMO) & ~CF_SHARE;
+                state = ST_SHADE;
+                return true;
+            }
+        }
+        fl = (!(a.flags & PT_FLAG_NO_PRIMARY_CACHE) && !lens) ? (fl | CF_PRIMARY) : (fl & ~CF_PRIMARY);
+        return begin_trace(kMaxFloat, -1.0f);
+    };
+    // begin the visibility ray of connection k
+    auto vis_stage = [&](uint32_t k, V3 xi, V3 xj) -> bool {
+        float len;
+        head_vis_ray(xi, xj, &ro, &rd, &len);
+        cu1 = len;
+        stage = (stage & ~0xfu) | HS_SH | (k << 2);
+        wave_count(lcnt + 1, lane);
+        return begin_trace(head_vis_bound(len), head_vis_occluded(len));
+    };
+    auto ldv = [&](int k) -> V3 { return u3f(R.ld4(k)); };
+    bool again = (state == ST_SHADE || state == ST_SLOW);
+    for (uint32_t iters = 0; iters < a.wf_iters; ++iters) {
+      if (again) {
+        again = false;
+        if (state == ST_SLOW) {
+            wave_count(lcnt + 3, lane);
+            SEC(SEC_SLOW);
+            trace_slow(ro, rd, a.root, a.nodes, a.tris_leaf, S.spill(), S.stride, a.cull_rel, a.cull_abs,
+                       &htri, &ht, kCount ? a.tri_counts : nullptr);
+        }
+        state = ST_SHADE;
+        take_hit();
+        for (;;) {   // consume the hit; advance until the lane needs a trace or its unit is done
+            SEC(SEC_BOUNCE);
+            bool sample_done = false;
+            C3 acc = c3(0, 0, 0);
+            if ((stage & 3u) == HS_T1) {
+                // light bounce hit x[1] (kernel.cu:266-287)
+                int32_t tri = htri;
+                float t = (float)((double)ht - 0.001);
+                if (t > kMaxFloat - 1) { tri = 0; t = 0; }
+                const V3 pos = ro + rd * t;
+                const V3 n2 = prim_normal(a, tri, pos);
+                const float G = __builtin_fabsf(dot(n2, rd)) / __builtin_fmaxf(0.001f, t * t);
+                const float ip1 = (float)(2 * 3.14159 / (double)G);
+                R.st4(HW_X1, __float_as_uint(pos.x), __float_as_uint(pos.y), __float_as_uint(pos.z), (uint32_t)prim_mat(a, tri));
+                R.st(HW_IP1, __float_as_uint(ip1));
+                R.st4(HW_N1, __float_as_uint(n2.x), __float_as_uint(n2.y), __float_as_uint(n2.z), 0u);
+                if (camera_stage()) {
+                    if (state == ST_SLOW) { again = true; break; }
+                    take_hit();
+                    continue;   // the camera hit is at hand (memo or a root miss)
+                }
+                break;
+            } else if ((stage & 3u) == HS_T2) {
+                // camera hit x[3] (kernel.cu:289-305)
+                int32_t tri = htri;
+                float t = (float)((double)ht - 0.001);
+                if (t > kMaxFloat - 1) { tri = 0; t = 0; }
+                const V3 x3 = ro + rd * t;
+                const V3 n3 = prim_normal(a, tri, x3);
+                R.st4(HW_X3, __float_as_uint(x3.x), __float_as_uint(x3.y), __float_as_uint(x3.z), (uint32_t)prim_mat(a, tri));
+                R.st4(HW_N3, __float_as_uint(n3.x), __float_as_uint(n3.y), __float_as_uint(n3.z), 0u);
+                // the camera bounce: cosine_ray (kernel.cu:78-99) with the draws taken at the start
+                SEC(SEC_COSINE);
+                const float r = sqrtf(cu1);
+                const float theta = (float)(2 * 3.14159 * (double)cu2);
+                float sn, cs;
+                det_sincos(theta, &sn, &cs);
+                const float y = sqrtf(__builtin_fmaxf(0.0f, 1.0f - cu1));
+                ro = x3;
+                rd = to_frame(n3, r * cs, y, r * sn);
+                stage = HS_T3;
+                wave_count(lcnt + 1, lane);
+                if (begin_trace(kMaxFloat, -1.0f)) {
+                    if (state == ST_SLOW) { again = true; break; }
+                    take_hit();
+                    continue;
+                }
+                break;
+            } else if ((stage & 3u) == HS_T3) {
+                // camera bounce hit x[2] (kernel.cu:324-350; decision d2: a miss is triangle 0, t 0)
+                int32_t tri = htri;
+                float t = (float)((double)ht - 0.001);
+                if (t > kMaxFloat - 1 || tri < 0) { tri = 0; t = 0; }
+                const uint4 c3v = R.ld4(HW_X0), c4 = R.ld4(HW_N0), c5 = R.ld4(HW_X1), c6 = R.ld4(HW_N1),
+                            c7 = R.ld4(HW_X3), c8 = R.ld4(HW_N3);
+                V3 x[4], nrm[4];
+                x[0] = u3f(c3v); nrm[0] = u3f(c4); x[1] = u3f(c5); nrm[1] = u3f(c6); x[3] = u3f(c7); nrm[3] = u3f(c8);
+                x[2] = ro + rd * t;
+                nrm[2] = prim_normal(a, tri, x[2]);
+                float G = __builtin_fabsf(dot(nrm[3], rd) * dot(nrm[2], rd)) / (t * t);
+                if (G == 0) G = 1;
+                if (G != G) G = 1;
+                const int32_t mat[4] = {(int32_t)c3v.w, (int32_t)c5.w, prim_mat(a, tri), (int32_t)c7.w};
+                const float ip[3] = {fresh(a.total_light_area), __uint_as_float(c4.w), (float)(3.14159 / (double)G)};
+                HeadGeo g;
+                head_geometry(x, nrm, g);
+                R.st4(HW_X2, __float_as_uint(x[2].x), __float_as_uint(x[2].y), __float_as_uint(x[2].z), __float_as_uint(g.G1));
+                R.st4(HW_GC, __float_as_uint(g.Gc[0]), __float_as_uint(g.Gc[1]), __float_as_uint(g.Gc[2]), __float_as_uint(g.Gc[3]));
+                R.st(HW_G3, __float_as_uint(g.G3));
+                R.st(HW_IP2, __float_as_uint(ip[2]));
+                R.st(HW_MAT2, (uint32_t)mat[2]);
+                uint32_t need = 0;
+                acc = head_weights(a, mat, ip, g, 0u, &need);
+                if (need == 0u) {
+                    sample_done = true;   // no connection needs a visibility ray: acc is the sample's radiance
+                } else {
+                    stage = (need << 8);
+                    const uint32_t k = (uint32_t)__builtin_ctz(need);
+                    // (the endpoints re-read from the record: the vertices need not stay live across the weights)
+                    asm volatile("" ::: "memory");
+                    if (vis_stage(k, ldv((k >> 1) ? HW_X1 : HW_X0), ldv((k & 1u) ? HW_X3 : HW_X2))) {
+                        if (state == ST_SLOW) { again = true; break; }
+                        take_hit();
+                        continue;
+                    }
+                    break;
+                }
+            } else {
+                // visibility ray of connection k (kernel.cu:397-405)
+                const uint32_t k = (stage >> 2) & 3u, need = (stage >> 8) & 15u;
+                if ((double)__builtin_fabsf(ht - cu1) <= 0.01) stage |= 1u << (4 + k);
+                const uint32_t rest = need & ~((2u << k) - 1u);
+                if (rest != 0u) {
+                    const uint32_t k2 = (uint32_t)__builtin_ctz(rest);
+                    const V3 xi = ldv((k2 >> 1) ? HW_X1 : HW_X0), xj = ldv((k2 & 1u) ? HW_X3 : HW_X2);
+                    if (vis_stage(k2, xi, xj)) {
+                        if (state == ST_SLOW) { again = true; break; }
+                        take_hit();
+                        continue;
+                    }
+                    break;
+                }
+                // the sample's last pass: the weights again, now with the visibility bits
+                HeadGeo g;
+                const uint4 gc = R.ld4(HW_GC);
+                g.Gc[0] = __uint_as_float(gc.x); g.Gc[1] = __uint_as_float(gc.y); g.Gc[2] = __uint_as_float(gc.z);
+                g.Gc[3] = __uint_as_float(gc.w);
+                g.G1 = __uint_as_float(R.ld(HW_G1));
+                g.G3 = __uint_as_float(R.ld(HW_G3));
+                const int32_t mat[4] = {(int32_t)R.ld(HW_MAT0), (int32_t)R.ld(HW_MAT1), (int32_t)R.ld(HW_MAT2), (int32_t)R.ld(HW_MAT3)};
+                const float ip[3] = {fresh(a.total_light_area), __uint_as_float(R.ld(HW_IP1)), __uint_as_float(R.ld(HW_IP2))};
+                acc = head_weights(a, mat, ip, g, (stage >> 4) & 15u, nullptr);
+                sample_done = true;
+            }
+            if (!sample_done) break;
+            // sample n's end: the running mean (kernel.cu:551-552), or the split pixel's per-sample slot
+            wave_count(lcnt + 2, lane);
+            SEC(SEC_SAMPLE_END);
+            const uint4 c13 = R.ld4(HW_PXY);
+            const uint32_t px = c13.x & 0xffffu, py = c13.x >> 16;
+            if (!(fl & CF_SPLIT)) {
+                const uint4 m01 = R.ld4(HW_M), m2 = R.ld4(HW_M + 4);
+                const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
+                const double x0 = dbl(m01.x, m01.y) * fn1, x1 = dbl(m01.z, m01.w) * fn1, x2 = dbl(m2.x, m2.y) * fn1;
+                double m0, mm1, mm2;
+                if (__ballot(!(quot_ok(x0) && quot_ok(x1) && quot_ok(x2) && quot_ok(acc.r) && quot_ok(acc.g) &&
+                               quot_ok(acc.b))) == 0ull) {
+                    const double rf = 1.0 / fn;
+                    m0 = div_mk_d(x0, fn, rf) + div_mk_d(acc.r, fn, rf);
+                    mm1 = div_mk_d(x1, fn, rf) + div_mk_d(acc.g, fn, rf);
+                    mm2 = div_mk_d(x2, fn, rf) + div_mk_d(acc.b, fn, rf);
+                } else {
+                    m0 = x0 / fn + acc.r / fn;
+                    mm1 = x1 / fn + acc.g / fn;
+                    mm2 = x2 / fn + acc.b / fn;
+                }
+                if (n >= a.spp) {
+                    float* o3 = a.out + out_pixel(a, px, py) * 3;
+                    o3[0] = (float)m0;
+                    o3[1] = (float)mm1;
+                    o3[2] = (float)mm2;
+                    state = ST_IDLE;
+                    break;
+                }
+                R.st4(HW_M, dlo(m0), dhi(m0), dlo(mm1), dhi(mm1));
+                R.st2(HW_M + 4, dlo(mm2), dhi(mm2));
+            } else {
+                double* Lb = a.lbuf + ((size_t)c13.y * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
+                Lb[0] = acc.r;
+                Lb[1] = acc.g;
+                Lb[2] = acc.b;
+                if ((uint32_t)n >= nend) {
+                    state = ST_IDLE;
+                    break;
+                }
+            }
+            ++n;
+            again = start_sample(px, py);
+            break;
+        }
+      }
+      if (iters != 0u) {
+          if (__ballot(again) == 0ull) break;
+          continue;
+      }
+      // refill: lanes whose unit is finished take the next units of this shard
+      uint64_t idle = __ballot(state == ST_IDLE);
+      if (idle) {
+          SEC(SEC_REFILL);
+          const uint32_t u = take_unit<kCount>(a, lane, idle, state == ST_IDLE, lprobe, done_rel);
+          if (state == ST_IDLE) {
+              if (u >= a.nunits) {
+                  if (a.lane_times) a.lane_times[R.voff >> 4] = wall_clock64();
+                  state = ST_DONE;
+              } else {
+                  const size_t N = a.nunits;
+                  const uint32_t pxy = a.pix_states[UW_PXY * N + u];
+                  if (pxy != kNoPixel) {
+                      const uint32_t n0 = a.pix_states[UW_N0 * N + u];
+                      rng.v0 = a.pix_states[u];
+                      rng.v1 = a.pix_states[N + u];
+                      rng.v2 = a.pix_states[2 * N + u];
+                      rng.v3 = a.pix_states[3 * N + u];
+                      rng.v4 = a.pix_states[4 * N + u];
+                      rng.d = a.pix_states[5 * N + u];
+                      nend = a.pix_states[UW_NEND * N + u];
+                      n = (int)(n0 & 0x7fffffffu);
+                      const bool split = u >= a.nwhole;
+                      fl = (n0 >> 31) ? CF_LENS : CF_CAMC;
+                      if (!(fl & CF_LENS))
+                          R.st4(HW_CD, a.pix_states[UW_CD * N + u], a.pix_states[(UW_CD + 1) * N + u],
+                                a.pix_states[(UW_CD + 2) * N + u], 0u);
+                      if (split) fl |= CF_SPLIT;
+                      if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
+                          fl |= (n == 1) ? CF_OWNER : CF_SHARE;
+                      R.st4(HW_PXY, pxy, split ? a.pix_states[UW_TQ * N + u] : 0u, 0u, 0u);
+                      R.st4(HW_M, 0u, 0u, 0u, 0u); R.st2(HW_M + 4, 0u, 0u);
+                      again = start_sample(pxy & 0xffffu, pxy >> 16);
+                  }
+              }
+          }
+      }
+      if (__ballot(again) == 0ull) break;
+    }
+    if (a.root_first && state == ST_TRACE && w.node == 0u) {
+        bool more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        for (uint32_t k = 1; more && k < a.root_first && w.node < S.ntop && !leaf4_pending(w); ++k)
+            more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        if (!more) {   // nothing below the bound: a miss
+            w.best_t = kMaxFloat;
+            state = ST_SHADE;
+        }
+    }
+    SEC(SEC_RECORD);
+    R.st4(HW_N, (uint32_t)n, stage, fl, rng.d);
+    R.st4(HW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
+    R.st4(HW_RNG_V4, rng.v4, nend, __float_as_uint(cu1), __float_as_uint(cu2));
+}
+
+// The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
+template <bool kCount, bool kHead>
+__device__ __forceinline__ void wf_main(const Args& a)
 {
     extern __shared__ uint32_t lds_wf[];
     // after the four waves' rings (kWaveLdsWords each): the block counters (traced, reference,
@@ -1431,7 +2002,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
     Stack4 S;
     S.ring = lds_wf + (threadIdx.x >> 6) * kWaveLdsWords + lane;
     S.stride = a.spill_stride;
-    const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kColdWords * a.cold_stride * 4u), 0x00020000),
+    constexpr uint32_t kRecWords = kHead ? (uint32_t)kHeadWords : (uint32_t)kColdWords;
+    const ColdRec R{__builtin_amdgcn_make_buffer_rsrc(a.cold, 0, (int)(kRecWords * a.cold_stride * 4u), 0x00020000),
                     (uint32_t)(blockIdx.x * blockDim.x + threadIdx.x) * 16u, a.cold_stride * 16u};
     S.spill_base = a.spill;   // spill column of lane g at byte offset 4g = R.voff / 4
     S.lane_off = &R.voff;
@@ -1445,7 +2017,20 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
             reinterpret_cast<float4*>(lprobe + 4 + kMaxProbeEmitters * 12)[k] = reinterpret_cast<const float4*>(a.lights)[k];
     for (uint32_t k = threadIdx.x; k < a.num_emis * 3; k += blockDim.x)
         reinterpret_cast<float4*>(lprobe + 4)[k] = reinterpret_cast<const float4*>(a.emis)[k];
-    float4* const ltop = reinterpret_cast<float4*>(reinterpret_cast<char*>(lprobe) + kProbeLdsBytes);
+    if (kHead && a.num_lights < kLdsLights) {   // integrator 1: each staged light's normal and material
+        float4* const lnm = reinterpret_cast<float4*>(lprobe + 4 + kMaxProbeEmitters * 12 + kLdsLights * 12);
+        for (uint32_t k = threadIdx.x; k <= a.num_lights; k += blockDim.x) {
+            const DLight& L = a.lights[k];
+            float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (L.pad == 0.0f) {
+                const DShade& sh = a.shade[L.tri];
+                q = make_float4(sh.nx, sh.ny, sh.nz, __uint_as_float((uint32_t)sh.mat));
+            }
+            lnm[k] = q;
+        }
+    }
+    float4* const ltop = reinterpret_cast<float4*>(reinterpret_cast<char*>(lprobe) + kProbeLdsBytes +
+                                                   (kHead ? kHeadLdsLightBytes : 0));
     for (uint32_t k = threadIdx.x; k < a.top_nodes * (kTopNodeBytes / 16); k += blockDim.x) {
         const uint32_t nd = k / (kTopNodeBytes / 16), q = k - nd * (kTopNodeBytes / 16);
         ltop[k] = reinterpret_cast<const float4*>(a.nodes4 + nd)[q];
@@ -1483,8 +2068,8 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
                 if (noleaf && deep == 0u) ++itc[5];
             }
             if (state == ST_TRACE) {
-                const bool more = walk4_step<kCount, true>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel, a.cull_abs,
-                                                           a.node_mask, cnt);
+                const bool more = walk4_step<kCount, true, NoSetup, kHead>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel,
+                                                                           a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
                     atomicAdd(lhist + min(31 - __clz((int)steps), kHist - 1), 1u);
@@ -1497,8 +2082,14 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // the winner's check against the reference BVH runs in the shading phase
         // (htri, ht) == (w.best_slot, w.best_t): the hit is already in place
         // (no winner: a miss -- or, for a bounded last-bounce walk, never expected: exact slow walk)
-        if (state == ST_WALKED)
-            state = (w.best_slot != kNone) ? ST_CHECK : (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
+        if (state == ST_WALKED) {
+            if (kHead) {   // integrator 1: no hit below the bound is a miss (a visibility walk's "not visible")
+                if (w.best_slot != kNone) state = ST_CHECK;
+                else { w.best_t = kMaxFloat; state = ST_SHADE; }
+            } else {
+                state = (w.best_slot != kNone) ? ST_CHECK : (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
+            }
+        }
 
         if (kCount) {
             const unsigned long long c = clock64();
@@ -1511,8 +2102,10 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         // words are read and written in the record where they are used.
         if (kCount) ++shade_slots;
         // (the lane id is recomputed for the shading pass: one VGPR less live across the walk loop)
-        if (state != ST_TRACE && state != ST_DONE)
-            shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel, cnt);
+        if (state != ST_TRACE && state != ST_DONE) {
+            if (kHead) shade_lane_head<kCount>(R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel, cnt);
+            else shade_lane<kCount>(a, R, (int)__lane_id(), state, ro, rd, htri, ht, w, S, lcnt, lprobe, done_rel, cnt);
+        }
         if (kCount) shade_clk += clock64() - clk0;
         if (__ballot(state != ST_DONE) == 0ull) break;
     }
@@ -1560,6 +2153,19 @@ __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
         const uint32_t v = reinterpret_cast<const uint32_t*>(lcnt + 4)[threadIdx.x];
         if (v) atomicAdd(a.counters + 32 + threadIdx.x, (unsigned long long)v);
     }
+}
+
+template <bool kCount, int kMinWaves>
+__global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
+{
+    wf_main<kCount, false>(a);
+}
+
+// integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the wavefront state machine
+template <bool kCount, int kMinWaves>
+__global__ __launch_bounds__(256, kMinWaves) void render_head_wf(Args a)
+{
+    wf_main<kCount, true>(a);
 }
 
 // ------------------------------------------------------------------ output step
@@ -1778,6 +2384,8 @@ struct pt_ctx {
                                     // (measured: 1/8 and 1/4 shards +3%, full frame and 1/2 neutral)
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
     uint32_t wf_top = kTopNodesMax; // BVH4 nodes staged in each block's LDS (PT_WF_TOP; 0 = none)
+    bool head_wf = true;            // integrator 1 on the wavefront kernel (PT_HEAD_WF=0: the tile kernel)
+    int head_min_waves = 4;         // its register budget (PT_HEAD_MIN_WAVES: 4 = 128 VGPRs, 5 = 96; 4 measured faster)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
@@ -1981,6 +2589,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_QUEUES")) c->wf_queues = (atoi(e) > 1) ? kQueues : 1u;
         if (const char* e = getenv("PT_JUMP_BYTES")) c->use_jump_bytes = atoi(e) != 0;
         if (const char* e = getenv("PT_TILE_FAST4")) c->tile_fast4 = atoi(e) != 0;
+        if (const char* e = getenv("PT_HEAD_WF")) c->head_wf = atoi(e) != 0;
+        if (const char* e = getenv("PT_HEAD_MIN_WAVES")) c->head_min_waves = (atoi(e) == 5) ? 5 : 4;
         if (const char* e = getenv("PT_WF_MIN_WAVES")) {
             const int v = atoi(e);
             c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
@@ -2354,7 +2964,9 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     // the render-path BVH's box margin assumes ray origins within ~2^6 of the scene extent
     const float cam_ext = std::fmax(std::fabs(cam->pos.x), std::fmax(std::fabs(cam->pos.y), std::fabs(cam->pos.z)));
     const bool near_cam = cam_ext <= 64.0f * c->scene_extent;
-    const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR) && !refwalk &&
+    // integrator 1 takes the wavefront kernel too (PT_HEAD_WF=0: the tile kernel, for comparisons)
+    const bool head = p->integrator == PT_INTEGRATOR_HEAD;
+    const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR || (head && c->head_wf)) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam &&
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
     HIP_TRY(hipMemsetAsync(c->counters, 0, kCounterWords * sizeof(unsigned long long), stream));
@@ -2381,10 +2993,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         b.stack_words = kRing * 64;
         b.node_mask = c->node4_mask;
         b.top_nodes = c->top_nodes;
+        b.head = head ? 1u : 0u;
         const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
-                              kProbeLdsBytes +
+                              kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0) +
                               (size_t)b.top_nodes * kTopNodeBytes;
-        uint32_t blocks = (uint32_t)c->num_cus * (c->wf_waves_per_cu / 4 ? c->wf_waves_per_cu / 4 : 1);
+        const uint32_t wpc = (head && !count) ? 4u * (uint32_t)c->head_min_waves : c->wf_waves_per_cu;
+        uint32_t blocks = (uint32_t)c->num_cus * (wpc / 4 ? wpc / 4 : 1);
         // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
         // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`
         // pixel slots are split into sample chunks, so the final units are short.
@@ -2489,7 +3103,8 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
             b.pmemo = c->pmemo;
         }
         const size_t per_lane = stack_words_per_lane(c);
-        if (int rc = ensure_spill(c, per_lane * (size_t)blocks * 256 + kColdWords * (size_t)blocks * paths_per_block))
+        const size_t rec_words = head ? (size_t)kHeadWords : (size_t)kColdWords;   // shading record per lane
+        if (int rc = ensure_spill(c, per_lane * (size_t)blocks * 256 + rec_words * (size_t)blocks * paths_per_block))
             return rc;
         b.spill = c->spill;
         b.spill_stride = blocks * 256;
@@ -2539,7 +3154,12 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         kernel_events = true;
         units = b.nunits;
         split = b.ntail;
-        if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        if (head) {
+            if (count) hipLaunchKernelGGL((render_head_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
+            else if (c->head_min_waves == 4) hipLaunchKernelGGL((render_head_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+            else hipLaunchKernelGGL((render_head_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        }
+        else if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);

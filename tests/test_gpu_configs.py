@@ -157,31 +157,59 @@ def test_wide_image_seeding_beyond_24_morton_bits(monkeypatch, jump_bytes):
     _check(s, img, cam_kw, w, h, spp, 3, pix)
 
 
-@pytest.mark.parametrize("fast4", ["1", "0"])
-def test_head_integrator_tile_walks_bit_identical(standin, monkeypatch, fast4):
-    """Integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the 262K stand-in: the tile
-    kernel tracing with the render-path BVH4 walk (default; winner check + exact slow walk) and
-    with the reference-BVH culled walk (PT_TILE_FAST4=0) render the same bits as the
-    reference-order walk, and a spread of pixels equals the oracle."""
+@pytest.mark.parametrize("mode", ["wavefront", "tile4", "tileref"])
+def test_head_integrator_walks_bit_identical(standin, monkeypatch, mode):
+    """Integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the 262K stand-in: the wavefront
+    state machine (default: T1 light bounce, T2 camera memo, T3 camera bounce, bounded visibility walks),
+    the tile kernel on the render-path BVH4 walk (PT_HEAD_WF=0) and on the reference-BVH culled walk
+    (PT_HEAD_WF=0 PT_TILE_FAST4=0) render the same bits as the reference-order walk, and a spread of
+    pixels equals the oracle."""
     s, r = standin
     w, h, spp = 160, 96, 4
     cam_kw = scenes.SPONZA_STANDIN_CAMERA
     cam = pt.make_camera(width=w, height=h, **cam_kw)
-    ref, _ = r.render(cam, w, h, spp, bounces=3, integrator=1, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
-    monkeypatch.setenv("PT_TILE_FAST4", fast4)
+    ref, sref = r.render(cam, w, h, spp, bounces=3, integrator=1, flags=pt.PT_FLAG_REFERENCE_TRAVERSAL)
+    if mode != "wavefront":
+        monkeypatch.setenv("PT_HEAD_WF", "0")
+        monkeypatch.setenv("PT_TILE_FAST4", "1" if mode == "tile4" else "0")
     with pt.Renderer(s, 0) as r2:
         img, st = r2.render(cam, w, h, spp, bounces=3, integrator=1)
     assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == sref["rays_reference"]
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
-    if fast4 == "1":
+    if mode == "wavefront":
+        assert st["work_units"] > 0   # (the wavefront kernel ran)
         import oracle
         osc = oracle.OracleScene(s.arrays())
         ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"], w, h)
         pix = _spread(w, h, 24, 6)
-        o, _ = oracle.render(osc, ocam, w, h, spp, 3, 1, 1234, pixels=pix)
+        o, cnt = oracle.render(osc, ocam, w, h, spp, 3, 1, 1234, pixels=pix)
         a = img.reshape(-1, 3)[pix]
         b = o.reshape(-1, 3)[pix].astype(np.float32)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_c3_head_integrator_full_frame(standin, monkeypatch):
+    """C3 (1920x1080, 256 spp) with integrator 1: the wavefront kernel (the measured path, with its
+    split units and bounded visibility walks) equals the tile kernel on every pixel, and a spread of
+    pixels equals the oracle."""
+    s, r = standin
+    w, h, spp = 1920, 1080, 256
+    cam_kw = scenes.SPONZA_STANDIN_CAMERA
+    cam = pt.make_camera(width=w, height=h, **cam_kw)
+    a, sa = r.render(cam, w, h, spp, bounces=3, integrator=1)
+    assert sa["work_units"] > w * h   # (split units in the tail)
+    monkeypatch.setenv("PT_HEAD_WF", "0")
+    with pt.Renderer(s, 0) as r2:
+        b, sb = r2.render(cam, w, h, spp, bounces=3, integrator=1)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa["rays_reference"] == sb["rays_reference"] and sa["samples"] == sb["samples"] == w * h * spp
+    import oracle
+    osc = oracle.OracleScene(s.arrays())
+    ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"], w, h)
+    pix = _spread(w, h, 256, 7)
+    o, _ = oracle.render(osc, ocam, w, h, spp, 3, 1, 1234, pixels=pix)
+    assert np.array_equal(a.reshape(-1, 3)[pix].view(np.uint32), o.reshape(-1, 3)[pix].astype(np.float32).view(np.uint32))
 
 
 def test_merged_shading_records_bit_identical(standin, monkeypatch):

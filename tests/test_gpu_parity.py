@@ -150,6 +150,33 @@ def test_sample_chunk_units_bit_exact(oracle_mod, monkeypatch, chunks, radius):
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("chunks,radius,tail", [("1", 0.0, None), ("3", 0.0, None), ("7", 0.05, None), ("2", 0.05, "100"),
+                                               ("4", 0.0, "37")])
+def test_head_wavefront_units_bit_exact(oracle_mod, monkeypatch, chunks, radius, tail):
+    """Integrator 1 on the wavefront kernel with sample-chunk work units: a chunk's XORWOW state is
+    fast-forwarded by the fixed 7 (+2 lens) draws per sample, its per-sample radiance combined in
+    order, the camera hit shared by the pixel's chunks (pinhole); lens draws per sample.  Shards of 3
+    sum to the same bits."""
+    monkeypatch.setenv("PT_WF_CHUNKS", chunks)
+    if tail is not None:
+        monkeypatch.setenv("PT_WF_TAIL_NPIX", tail)
+    s = load_scene("cornell_blob")
+    w, h, spp = 24, 16, 9
+    cam = pt.make_camera(pos=CAM["pos"], dist_from_film=1.0, focal_length=3.0, radius=radius, width=w, height=h)
+    with pt.Renderer(s, 0) as r:
+        img, st = r.render(cam, w, h, spp, bounces=3, integrator=1)
+        parts = np.zeros_like(img)
+        for k in range(3):
+            part, _ = r.render(cam, w, h, spp, bounces=3, integrator=1, shard_index=k, shard_count=3)
+            parts += part
+    ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, 1, radius=radius)
+    assert _bits_equal(img, ref) == 0
+    assert _bits_equal(parts, img.astype(np.float64)) == 0
+    assert st["samples"] == w * h * spp
+    assert st["rays_reference"] == cnt["traces"]
+    assert st["work_units"] >= w * h
+
+
 @pytest.mark.parametrize("tail,chunks,radius", [("100", "3", 0.0), ("1", "9", 0.0), ("383", "2", 0.05),
                                                ("0", "4", 0.0)])
 def test_tail_split_units_bit_exact(oracle_mod, monkeypatch, tail, chunks, radius):
