@@ -208,17 +208,23 @@ class FrameLoop:
     issued asynchronously so that it overlaps the next frame's render (a buffer is zeroed again
     only after its reduce has completed -- `wait()` orders the stream, the host does not block).
 
-    render(buf) -> stats dict: renders this rank's tiles into the zero-filled buf.
+    render(buf) -> stats dict: renders this rank's tiles into the zero-filled buf -- or, with `wait`
+    given, only enqueues the render (pt_render_device_async) and wait() returns the oldest queued
+    frame's stats: frame k+1 is queued before frame k's stats are collected, so the GPU never idles
+    between frames (the host's return path and the next launches overlap the render).
     reduce(buf) -> work with .wait(), or None (one process, or a synchronous reduce).
-    Every frame is rendered and reduced in full; `drain()` returns the last frame's buffer once its
-    reduce is ordered before whatever the caller does next."""
+    step() returns a frame's stats (the previous frame's when asynchronous, None for the first);
+    `drain()` returns (the last frame's buffer once its reduce is ordered before whatever the caller
+    does next, the stats of the frames still in flight)."""
 
-    def __init__(self, bufs, render, reduce=None):
+    def __init__(self, bufs, render, reduce=None, wait=None):
         self.bufs = list(bufs)
         self.render = render
         self.reduce = reduce
+        self.wait = wait
         self.pending = [None] * len(self.bufs)
         self.frames = 0
+        self.inflight = 0
 
     def step(self):
         k = self.frames % len(self.bufs)
@@ -231,14 +237,24 @@ class FrameLoop:
         if self.reduce is not None:
             self.pending[k] = self.reduce(buf)
         self.frames += 1
-        return st
+        if self.wait is None:
+            return st
+        self.inflight += 1
+        if self.inflight > 1:   # the previous frame's stats, with this one queued behind it
+            self.inflight -= 1
+            return self.wait()
+        return None
 
     def drain(self):
+        stats = []
+        while self.wait is not None and self.inflight > 0:
+            stats.append(self.wait())
+            self.inflight -= 1
         for k, w in enumerate(self.pending):
             if w is not None:
                 w.wait()
                 self.pending[k] = None
-        return self.bufs[(self.frames - 1) % len(self.bufs)] if self.frames else self.bufs[0]
+        return (self.bufs[(self.frames - 1) % len(self.bufs)] if self.frames else self.bufs[0]), stats
 
 
 def make_reduce(dist, backend, rank):
@@ -281,6 +297,8 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="skip the counting pass (roofline bytes)")
     ap.add_argument("--sim-shards", type=int, default=1,
                     help="diagnostic, single process only: render shard 0 of N (one GPU's share at N GPUs)")
+    ap.add_argument("--sync-frames", action="store_true",
+                    help="one blocking render per frame (pt_render_device) instead of frames queued back to back")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
@@ -329,7 +347,14 @@ def main():
         return r.render_device(cam, buf.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
                                flags=args.flags | flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
 
-    loop = FrameLoop(fbs, render, make_reduce(dist, backend, rank) if distributed else None)
+    def render_async(buf):
+        r.render_device_async(cam, buf.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
+                              flags=args.flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
+
+    if args.sync_frames:
+        loop = FrameLoop(fbs, render, make_reduce(dist, backend, rank) if distributed else None)
+    else:
+        loop = FrameLoop(fbs, render_async, make_reduce(dist, backend, rank) if distributed else None, wait=r.wait)
 
     # counting pass (same inputs, counting variant): algorithmic bytes of the render kernel
     counts = None
@@ -347,9 +372,11 @@ def main():
     stats = []
     for _ in range(args.steps):
         st = loop.step()
-        kernel_ms.append(st["kernel_ms"])
-        stats.append(st)
-    fb = loop.drain()
+        if st is not None:
+            stats.append(st)
+    fb, rest = loop.drain()
+    stats += rest
+    kernel_ms = [st["kernel_ms"] for st in stats]
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()

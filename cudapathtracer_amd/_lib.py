@@ -108,6 +108,8 @@ SIGNATURES = {
     "pt_render": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.POINTER(Stats)]),
     "pt_render_device": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.c_void_p,
                                    C.POINTER(Stats)]),
+    "pt_render_device_async": (C.c_int, [C.c_void_p, C.POINTER(Params), C.POINTER(Camera), C.c_void_p, C.c_void_p]),
+    "pt_render_wait": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "pt_trace": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "pt_trace_counts": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                   C.c_void_p, C.POINTER(C.c_uint64)]),

@@ -251,6 +251,21 @@ class Renderer:
                                          None if stream_ptr is None else C.c_void_p(int(stream_ptr)), C.byref(st)))
         return st.as_dict()
 
+    def render_device_async(self, cam, d_out_ptr, width, height, spp, bounces=3, integrator=0, seed=1234, flags=0,
+                            shard_index=0, shard_count=1, stream_ptr=None, pixel_order=0, tile_w=0, tile_h=0):
+        """Enqueue render_device's work on the stream and return at once (at most 2 in flight); collect
+        the stats of the oldest with wait()."""
+        p = self.params(width, height, spp, bounces, integrator, seed, flags, shard_index, shard_count,
+                        pixel_order, tile_w, tile_h)
+        L.check(L.lib().pt_render_device_async(self._h, C.byref(p), C.byref(cam), C.c_void_p(int(d_out_ptr)),
+                                               None if stream_ptr is None else C.c_void_p(int(stream_ptr))))
+
+    def wait(self):
+        """Stats dict of the oldest render in flight (render_device_async), once it has finished."""
+        st = L.Stats()
+        L.check(L.lib().pt_render_wait(self._h, C.byref(st)))
+        return st.as_dict()
+
     def tonemap(self, img):
         """Output step on the GPU: (H, W, 3) float32 mean image -> int32 codes equal to
         pt_tonemap_u8 (kernel.cu:763-778) per channel."""

@@ -712,6 +712,7 @@ __device__ __forceinline__ uint32_t dhi(double v) { return (uint32_t)__double2hi
 enum : uint32_t { UW_PXY = 6, UW_N0, UW_NEND, UW_TQ, UW_CD, kUnitWords = UW_CD + 3 };
 constexpr uint32_t kNoPixel = 0xffffffffu;   // UW_PXY of a slot outside the image
 constexpr uint32_t kNoUnit = 0xffffffffu;
+constexpr int kCounterWords = 96;   // counters[]: 0..63 as listed, 64..95 the tail bins
 constexpr uint32_t kQueues = 8;              // unit counters (Args::unit_queues > 1)
 constexpr uint32_t kQueueBlock = 64;         // units per block of a counter's class
 constexpr uint32_t kQueueStride = 32;        // words between the counters (one 128-B line each)
@@ -752,9 +753,19 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     // at the start of every chunk, with everything else a lane needs to start the unit (pixel,
     // sample range, pinhole camera ray): the refill in the render kernel is then a few loads
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (blockIdx.x == 0) {   // this render's counters, unit counters and wall-clock minima (no memset launches)
+        for (uint32_t k = threadIdx.x; k < (uint32_t)kCounterWords; k += 256u)
+            a.counters[k] = (k == 20u || k == 21u) ? ~0ull : 0ull;
+        for (uint32_t k = threadIdx.x; k < kQueueStride * (kQueues + 1); k += 256u) a.pixel_counter[k] = 0u;
+        if (threadIdx.x < 4) a.tile_counter[threadIdx.x] = 0u;
+    }
     if (q >= a.npix) return;
     const bool split = q >= a.nwhole;
     const uint32_t t = q - a.nwhole;   // split slot (row of the per-sample buffer)
+    if (split) {   // its primary-hit word (pmemo): none yet
+        a.pmemo[2 * t] = 0u;
+        a.pmemo[2 * t + 1] = 0u;
+    }
     const bool mid = split && t < a.nmid;
     const uint32_t f0 = a.ntail - a.nfin;   // first slot of the final grade
     const bool fin = split && t >= f0;
@@ -911,7 +922,6 @@ __device__ __forceinline__ void wave_count(unsigned long long* c, int lane)
 enum : int { SEC_PASS = 0, SEC_CHECK, SEC_SLOW, SEC_BOUNCE, SEC_EMIT, SEC_COSINE, SEC_LIGHT, SEC_SAMPLE_END,
              SEC_START, SEC_CAMERA, SEC_DEAD, SEC_BEGIN, SEC_REFILL, SEC_MEMO, SEC_RECORD, SEC_PROBE, kSections = 16 };
 constexpr int kHist = 16;   // counting variant: walk steps per ray, log2 buckets (counters[48 + b])
-constexpr int kCounterWords = 96;   // counters[]: 0..63 as listed, 64..95 the tail bins
 constexpr int kTailBins = 16;   // counting variant: lane end / wave exit times after the queue drained,
                                 // bin k = [10 us x 2^(k-1), 10 us x 2^k) of the 100-MHz wall clock (bin 0: < 10 us)
 __device__ __forceinline__ uint32_t tail_bin(unsigned long long ticks)
@@ -2358,8 +2368,22 @@ struct pt_ctx {
     float scene_extent = 1.0f;
     void* pinned = nullptr;                    // pt_render: pinned staging buffer of the image copy-out
     size_t pinned_bytes = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the whole render
-    hipEvent_t ek0 = nullptr, ek1 = nullptr;   // the integration kernel alone
+    // renders in flight (pt_render_device_async / pt_render_wait): a FIFO of kFlights slots, each with
+    // its events and a pinned host copy of the render's counters
+    struct Flight {
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the whole render
+        hipEvent_t ek0 = nullptr, ek1 = nullptr;   // the integration kernel alone
+        hipEvent_t done = nullptr;                 // after the counters' copy
+        unsigned long long* hcnt = nullptr;        // pinned: the counters, copied behind the render
+        bool kernel_events = false, count = false;
+        uint64_t units = 0, split = 0;
+        int32_t spp = 0, bounces = 0;
+    };
+    static constexpr int kFlights = 2;
+    Flight fl[kFlights];
+    int fl_head = 0, fl_n = 0;                 // oldest in-flight slot, number in flight
+    uint64_t seed_cached = 0;                  // the seed seed_states was built for
+    bool seed_valid = false;
     int num_cus = 256;
     uint32_t* pixel_counter = nullptr;
     bool scene_fast = false;
@@ -2420,6 +2444,18 @@ static size_t stack_words_per_lane(const pt_ctx* c);
 static int ensure_spill(pt_ctx* c, size_t words);
 
 extern "C" {
+
+static bool create_flights(pt_ctx* c)
+{
+    for (pt_ctx::Flight& f : c->fl) {
+        if (hipEventCreate(&f.ev0) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
+            hipEventCreate(&f.ek0) != hipSuccess || hipEventCreate(&f.ek1) != hipSuccess ||
+            hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&f.hcnt), kCounterWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+            return false;
+    }
+    return true;
+}
 
 pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
 {
@@ -2835,8 +2871,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if (hipMalloc(reinterpret_cast<void**>(&c->counters), kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), kQueueStride * (kQueues + 1) * 4) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ek0) != hipSuccess || hipEventCreate(&c->ek1) != hipSuccess) {
+        !create_flights(c)) {
         pt_destroy(c);
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
     }
@@ -2856,10 +2891,11 @@ void pt_destroy(pt_ctx* c)
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     pt::free_pinned(c->pinned);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->ek0) (void)hipEventDestroy(c->ek0);
-    if (c->ek1) (void)hipEventDestroy(c->ek1);
+    for (pt_ctx::Flight& f : c->fl) {
+        for (hipEvent_t e : {f.ev0, f.ev1, f.ek0, f.ek1, f.done})
+            if (e) (void)hipEventDestroy(e);
+        if (f.hcnt) (void)hipHostFree(f.hcnt);
+    }
     delete c;
 }
 
@@ -2892,9 +2928,11 @@ static void write_lane_timing(const char* path, const std::vector<unsigned long 
     }
 }
 
-int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* d_out, void* stream_v, pt_stats* st)
+int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* d_out, void* stream_v)
 {
     if (!c || !p || !cam || !d_out) return pt::fail(PT_E_INVALID, "pt_render: null argument");
+    if (c->fl_n >= pt_ctx::kFlights)
+        return pt::fail(PT_E_INVALID, "pt_render_device_async: %d renders in flight (pt_render_wait first)", c->fl_n);
     if (p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 65535)
         return pt::fail(PT_E_INVALID, "pt_render: image size %dx%d out of range (1..65535)", p->width, p->height);
     if (p->spp < 0) return pt::fail(PT_E_INVALID, "pt_render: spp < 0");
@@ -2969,21 +3007,27 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR || (head && c->head_wf)) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam &&
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
-    HIP_TRY(hipMemsetAsync(c->counters, 0, kCounterWords * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
+    pt_ctx::Flight& F = c->fl[(c->fl_head + c->fl_n) % pt_ctx::kFlights];
+    if (c->fl_n > 0)   // (a render in flight on another stream still uses the context's buffers)
+        HIP_TRY(hipStreamWaitEvent(stream, c->fl[(c->fl_head + c->fl_n - 1) % pt_ctx::kFlights].done, 0));
+    // (the wavefront path's init_pixel_states resets the counters itself: one launch less per frame)
+    if (!(p->spp > 0 && a.ntiles_shard > 0 && wavefront)) {
+        HIP_TRY(hipMemsetAsync(c->counters, 0, kCounterWords * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
+        HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
+        HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
+    }
     if (count && (p->flags & PT_FLAG_TRI_COUNTS)) {   // per-triangle test counts of this render (pt_tri_counts)
         HIP_TRY(hipMemsetAsync(c->tri_counts, 0, (size_t)std::max<uint32_t>(c->num_tris, 1u) * 4, stream));
         a.tri_counts = c->tri_counts;
     }
-    HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
-    HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
     const uint32_t waves_per_cu = 16;
     uint32_t grid = (uint32_t)c->num_cus * waves_per_cu;
     if (grid > a.ntiles_shard * a.tile_blocks) grid = a.ntiles_shard > 0 ? a.ntiles_shard * a.tile_blocks : 1;
     // the tile kernel traces with the render-path BVH4 walk under the wavefront kernel's conditions
     // (PT_TILE_FAST4=0: the reference-BVH culled walk, as before)
     a.tile_fast4 = (!refwalk && !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam && c->tile_fast4 && c->num_tris > 0) ? 1u : 0u;
-    HIP_TRY(hipEventRecord(c->ev0, stream));
+    HIP_TRY(hipEventRecord(F.ev0, stream));
     bool kernel_events = false;   // ek0/ek1 recorded around the integration kernel (wavefront path)
     uint64_t units = 0, split = 0;
     if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
@@ -3099,7 +3143,6 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pmemo), mw * 4));
                 c->pmemo_words = mw;
             }
-            HIP_TRY(hipMemsetAsync(c->pmemo, 0, mw * 4, stream));
             b.pmemo = c->pmemo;
         }
         const size_t per_lane = stack_words_per_lane(c);
@@ -3145,12 +3188,16 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
                 c->jump_bytes = jb;
                 c->seed_states = ss;
             }
-            hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, c->seed_states);
+            if (!c->seed_valid || c->seed_cached != p->seed) {   // (depends on the seed only: kept across renders)
+                hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, c->seed_states);
+                c->seed_cached = p->seed;
+                c->seed_valid = true;
+            }
             b.jump_bytes = c->jump_bytes;
             b.seed_states = c->seed_states;
         }
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
-        HIP_TRY(hipEventRecord(c->ek0, stream));
+        HIP_TRY(hipEventRecord(F.ek0, stream));
         kernel_events = true;
         units = b.nunits;
         split = b.ntail;
@@ -3165,7 +3212,7 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ek1, stream));
+        HIP_TRY(hipEventRecord(F.ek1, stream));
         if (b.ntail > 0) hipLaunchKernelGGL(finalize_pixels, dim3((b.ntail + 255) / 256), dim3(256), 0, stream, b);
         HIP_TRY(hipGetLastError());
         if (d_times) {
@@ -3191,11 +3238,31 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
 #undef PT_LAUNCH
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(c->ev1, stream));
-    unsigned long long cnt[kCounterWords];
-    HIP_TRY(hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (count) {
+    HIP_TRY(hipEventRecord(F.ev1, stream));
+    HIP_TRY(hipMemcpyAsync(F.hcnt, c->counters, kCounterWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipEventRecord(F.done, stream));
+    F.kernel_events = kernel_events;
+    F.count = count;
+    F.units = units;
+    F.split = split;
+    F.spp = p->spp;
+    F.bounces = p->bounces;
+    ++c->fl_n;
+    return PT_OK;
+}
+
+int pt_render_wait(pt_ctx* c, pt_stats* st)
+{
+    if (!c) return pt::fail(PT_E_INVALID, "pt_render_wait: null context");
+    if (c->fl_n == 0) return pt::fail(PT_E_INVALID, "pt_render_wait: no render in flight");
+    HIP_TRY(hipSetDevice(c->device));
+    pt_ctx::Flight& F = c->fl[c->fl_head];
+    c->fl_head = (c->fl_head + 1) % pt_ctx::kFlights;
+    --c->fl_n;
+    // (the counters' copy is the render's last operation on its stream)
+    HIP_TRY(hipEventSynchronize(F.done));
+    const unsigned long long* cnt = F.hcnt;
+    if (F.count) {
         if (const char* path = getenv("PT_SECTION_DUMP")) {   // counting runs: shading section profile
             if (FILE* f = fopen(path, "a")) {
                 fprintf(f, "sections");
@@ -3218,14 +3285,14 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         }
     }
     float ms = 0.0f, kms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    if (kernel_events) HIP_TRY(hipEventElapsedTime(&kms, c->ek0, c->ek1));
+    HIP_TRY(hipEventElapsedTime(&ms, F.ev0, F.ev1));
+    if (F.kernel_events) HIP_TRY(hipEventElapsedTime(&kms, F.ek0, F.ek1));
     else kms = ms;   // (the tile kernel is the render's only launch)
     if (st) {
         st->seconds = ms * 1e-3;
         st->kernel_ms = kms;
-        st->work_units = units;
-        st->split_pixels = split;
+        st->work_units = F.units;
+        st->split_pixels = F.split;
         st->rays_traced = cnt[0];
         st->rays_reference = cnt[1];
         st->node_tests = cnt[2];
@@ -3239,10 +3306,18 @@ int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float*
         st->shade_cycles = cnt[10];
         st->spill_entries = cnt[25];
         st->lds_node_tests = cnt[13];
-        const uint64_t shard_px = cnt[4] / (uint64_t)(p->spp > 0 ? p->spp : 1);
-        st->rays_nominal = shard_px * (uint64_t)p->spp * (uint64_t)(p->bounces + 1);
+        const uint64_t shard_px = cnt[4] / (uint64_t)(F.spp > 0 ? F.spp : 1);
+        st->rays_nominal = shard_px * (uint64_t)F.spp * (uint64_t)(F.bounces + 1);
     }
     return PT_OK;
+}
+
+int pt_render_device(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* d_out, void* stream, pt_stats* st)
+{
+    if (c && c->fl_n > 0)
+        return pt::fail(PT_E_INVALID, "pt_render_device: %d asynchronous renders in flight (pt_render_wait first)", c->fl_n);
+    if (int rc = pt_render_device_async(c, p, cam, d_out, stream)) return rc;
+    return pt_render_wait(c, st);
 }
 
 }  // extern "C"
@@ -3338,6 +3413,7 @@ extern "C" int pt_tri_counts(pt_ctx* c, uint32_t* counts, uint32_t n)
 {
     pt::clear_error();
     if (!c || !counts) return pt::fail(PT_E_INVALID, "pt_tri_counts: null argument");
+    if (c->fl_n > 0) return pt::fail(PT_E_INVALID, "pt_tri_counts: renders in flight (pt_render_wait first)");
     if (n != c->num_tris) return pt::fail(PT_E_INVALID, "pt_tri_counts: n = %u, the scene has %u triangles", n, c->num_tris);
     if (n == 0) return PT_OK;
     HIP_TRY(hipSetDevice(c->device));
@@ -3350,6 +3426,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
 {
     pt::clear_error();
     if (!c) return pt::fail(PT_E_INVALID, "pt_trace: null context");
+    if (c->fl_n > 0) return pt::fail(PT_E_INVALID, "pt_trace: renders in flight (pt_render_wait first)");
     if (n == 0) return PT_OK;
     if (!rays || !tri_out || !t_out) return pt::fail(PT_E_INVALID, "pt_trace: null buffer");
     HIP_TRY(hipSetDevice(c->device));

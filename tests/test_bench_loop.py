@@ -45,6 +45,20 @@ def stub_render(rank, world, counter):
     return render
 
 
+def async_stub(render):
+    """render as pt_render_device_async / pt_render_wait present it: enqueue (here: do) the frame, hand
+    its stats out later, oldest first, at most two in flight."""
+    queue = []
+
+    def enqueue(buf):
+        assert len(queue) < 2, "at most two renders in flight per context"
+        queue.append(render(buf))
+
+    def wait():
+        return queue.pop(0)
+    return enqueue, wait
+
+
 class LazyReduce:
     """An async 'collective' that only lands at wait(): catches a loop that reuses a buffer before
     its reduce completed or returns a buffer whose reduce is still pending."""
@@ -63,14 +77,20 @@ class LazyReduce:
         return Work()
 
 
-def test_frame_loop_orders_buffers_and_reduces():
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_frame_loop_orders_buffers_and_reduces(asynchronous):
     counter = [0]
     log = []
     bufs = [torch.zeros((H, W, 3)) for _ in range(2)]
-    loop = bench.FrameLoop(bufs, stub_render(0, 1, counter), LazyReduce(log))
-    for _ in range(5):
-        loop.step()
-    out = loop.drain()
+    if asynchronous:
+        enqueue, wait = async_stub(stub_render(0, 1, counter))
+        loop = bench.FrameLoop(bufs, enqueue, LazyReduce(log), wait=wait)
+    else:
+        loop = bench.FrameLoop(bufs, stub_render(0, 1, counter), LazyReduce(log))
+    stats = [loop.step() for _ in range(5)]
+    out, rest = loop.drain()
+    stats = [st for st in stats if st is not None] + rest
+    assert len(stats) == 5 and all(st["samples"] == W * H for st in stats)
     assert counter[0] == 5 and len(log) == 5
     np.testing.assert_array_equal(out.numpy(), 2 * frame_image(4))
     # each reduce saw a complete frame: frame k's buffer was not zeroed under it
@@ -87,7 +107,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, frames, outdir):
+def _worker(rank, world, port, frames, outdir, asynchronous=False):
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
     import bench as b
@@ -95,10 +115,15 @@ def _worker(rank, world, port, frames, outdir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     counter = [0]
-    loop = b.FrameLoop([torch.zeros((H, W, 3)) for _ in range(2)], stub_render(rank, world, counter),
-                       b.make_reduce(dist, "gloo", rank))
+    bufs = [torch.zeros((H, W, 3)) for _ in range(2)]
+    if asynchronous:
+        enqueue, wait = async_stub(stub_render(rank, world, counter))
+        loop = b.FrameLoop(bufs, enqueue, b.make_reduce(dist, "gloo", rank), wait=wait)
+    else:
+        loop = b.FrameLoop(bufs, stub_render(rank, world, counter), b.make_reduce(dist, "gloo", rank))
     stats = [loop.step() for _ in range(frames)]
-    fb = loop.drain()
+    fb, rest = loop.drain()
+    stats = [st for st in stats if st is not None] + rest
     tot = torch.tensor([sum(s["samples"] for s in stats), sum(s["rays_traced"] for s in stats)], dtype=torch.float64)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     if rank == 0:
@@ -109,10 +134,10 @@ def _worker(rank, world, port, frames, outdir):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_frame_loop_assembles_every_frame(tmp_path, world):
+@pytest.mark.parametrize("world,asynchronous", [(2, False), (3, False), (2, True)])
+def test_gloo_frame_loop_assembles_every_frame(tmp_path, world, asynchronous):
     frames = 3
-    mp.spawn(_worker, args=(world, _free_port(), frames, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), frames, str(tmp_path), asynchronous), nprocs=world, join=True)
     fb = np.load(str(tmp_path / "fb.npy"))
     np.testing.assert_array_equal(fb, frame_image(frames - 1))
     tot = np.load(str(tmp_path / "tot.npy"))

@@ -455,3 +455,33 @@ def test_group_render_multi_device_equals_render():
     finally:
         for r in rs:
             r.close()
+
+
+def test_async_renders_queue_back_to_back(cb):
+    """pt_render_device_async / pt_render_wait: two frames queued on one stream (different shards, one
+    with the other integrator), collected oldest first -- the same bits and stats as blocking renders;
+    a third enqueue and a blocking render are refused while two are in flight."""
+    import torch
+    s, r = cb
+    w, h, spp = 40, 24, 3
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    ref0, st0 = r.render(cam, w, h, spp, bounces=3, shard_index=0, shard_count=2)
+    ref1, st1 = r.render(cam, w, h, spp, bounces=3, integrator=1, shard_index=1, shard_count=2)
+    a = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+    b = torch.zeros_like(a)
+    stream = torch.cuda.current_stream().cuda_stream
+    r.render_device_async(cam, a.data_ptr(), w, h, spp, bounces=3, shard_index=0, shard_count=2, stream_ptr=stream)
+    r.render_device_async(cam, b.data_ptr(), w, h, spp, bounces=3, integrator=1, shard_index=1, shard_count=2,
+                          stream_ptr=stream)
+    with pytest.raises(pt.PtError):
+        r.render_device_async(cam, b.data_ptr(), w, h, spp, stream_ptr=stream)
+    with pytest.raises(pt.PtError):
+        r.render(cam, w, h, spp)
+    sa = r.wait()
+    sb = r.wait()
+    with pytest.raises(pt.PtError):
+        r.wait()
+    assert np.array_equal(a.cpu().numpy().view(np.uint32), ref0.view(np.uint32))
+    assert np.array_equal(b.cpu().numpy().view(np.uint32), ref1.view(np.uint32))
+    for k in ("samples", "rays_traced", "rays_reference", "work_units"):
+        assert sa[k] == st0[k] and sb[k] == st1[k]
