@@ -1593,7 +1593,10 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
 {
     const Args& a = kernel_args_opaque();
     SEC(SEC_PASS);
-    const uint4 k0 = R.ld4(HW_N), k1 = R.ld4(HW_RNG_V0), k2 = R.ld4(HW_RNG_V4);
+    // (the XORWOW words v0..v3 are read and written only where a sample starts -- the only place a
+    // sample draws -- so they are not live across the pass: the shading code then fits 96 VGPRs)
+    const uint4 k0 = R.ld4(HW_N);
+    const uint32_t k2z = R.ld(HW_CU1);
     if (state == ST_CHECK) {
         SEC(SEC_CHECK);
         const float4 C = a.acc_tris[htri].c;
@@ -1604,9 +1607,10 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     int n = (int)k0.x;
     uint32_t stage = k0.y, fl = k0.z;
     Rng rng;
-    rng.d = k0.w; rng.v0 = k1.x; rng.v1 = k1.y; rng.v2 = k1.z; rng.v3 = k1.w; rng.v4 = k2.x;
-    uint32_t nend = k2.y;
-    float cu1 = __uint_as_float(k2.z), cu2 = __uint_as_float(k2.w);
+    rng.d = k0.w;
+    // (likewise v4, the unit end and the cosine draws: each read where it is used, written where it
+    // changes; only cell 0 -- n, stage, flags, XORWOW d -- is live across the pass)
+    float cu1 = __uint_as_float(k2z);   // the pending visibility ray's length (its check below)
     // (the staged light records and, behind them, each one's normal and material)
     const DLight* const llt = reinterpret_cast<const DLight*>(lprobe + 4 + kMaxProbeEmitters * 12);
     const float4* const lnm = reinterpret_cast<const float4*>(lprobe + 4 + kMaxProbeEmitters * 12 + kLdsLights * 12);
@@ -1641,8 +1645,13 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
         }
     };
     // start sample n: all of its draws, the light vertex, the camera ray of a lens sample; trace T1
-    auto start_sample = [&](uint32_t px, uint32_t py) -> bool {
+    auto start_sample = [&](uint32_t px, uint32_t py, bool have_rng) -> bool {
         SEC(SEC_START);
+        if (!have_rng) {
+            const uint4 k1 = R.ld4(HW_RNG_V0);
+            rng.v0 = k1.x; rng.v1 = k1.y; rng.v2 = k1.z; rng.v3 = k1.w;
+            rng.v4 = R.ld(HW_RNG_V4);
+        }
         const bool lens = (fl & CF_LENS) != 0u;
         float lu1 = 0.0f, lu2 = 0.0f;
         if (lens) { lu1 = rng_uniform(rng); lu2 = rng_uniform(rng); }   // drawPixel's cameraRay (kernel.cu:547)
@@ -1687,8 +1696,11 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
         }
         ro = p + n0 * 0.001f;                 // x[0] (kernel.cu:259)
         rd = rand_ray(n0, rng);               // the light bounce (kernel.cu:264)
-        cu1 = rng_uniform(rng);               // cosine_ray's draws for T3 (kernel.cu:307)
-        cu2 = rng_uniform(rng);
+        const float du1 = rng_uniform(rng);   // cosine_ray's draws for T3 (kernel.cu:307)
+        const float du2 = rng_uniform(rng);
+        R.st(HW_RNG_V4, rng.v4);
+        R.st2(HW_CU1, __float_as_uint(du1), __float_as_uint(du2));
+        R.st4(HW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
         R.st4(HW_X0, __float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), (uint32_t)m0);
         R.st4(HW_N0, __float_as_uint(n0.x), __float_as_uint(n0.y), __float_as_uint(n0.z), 0u);
         if (lens) {   // this sample's camera ray (its draws came first)
@@ -1740,7 +1752,8 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     auto vis_stage = [&](uint32_t k, V3 xi, V3 xj) -> bool {
         float len;
         head_vis_ray(xi, xj, &ro, &rd, &len);
-        cu1 = len;
+        cu1 = len;   // (its walk may end in this pass: a root miss, no triangles)
+        R.st(HW_CU1, __float_as_uint(len));
         stage = (stage & ~0xfu) | HS_SH | (k << 2);
         wave_count(lcnt + 1, lane);
         return begin_trace(head_vis_bound(len), head_vis_occluded(len));
@@ -1791,11 +1804,13 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 R.st4(HW_N3, __float_as_uint(n3.x), __float_as_uint(n3.y), __float_as_uint(n3.z), 0u);
                 // the camera bounce: cosine_ray (kernel.cu:78-99) with the draws taken at the start
                 SEC(SEC_COSINE);
-                const float r = sqrtf(cu1);
-                const float theta = (float)(2 * 3.14159 * (double)cu2);
+                const uint2 cc = R.ld2(HW_CU1);
+                const float du1 = __uint_as_float(cc.x), du2 = __uint_as_float(cc.y);
+                const float r = sqrtf(du1);
+                const float theta = (float)(2 * 3.14159 * (double)du2);
                 float sn, cs;
                 det_sincos(theta, &sn, &cs);
-                const float y = sqrtf(__builtin_fmaxf(0.0f, 1.0f - cu1));
+                const float y = sqrtf(__builtin_fmaxf(0.0f, 1.0f - du1));
                 ro = x3;
                 rd = to_frame(n3, r * cs, y, r * sn);
                 stage = HS_T3;
@@ -1909,13 +1924,13 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 Lb[0] = acc.r;
                 Lb[1] = acc.g;
                 Lb[2] = acc.b;
-                if ((uint32_t)n >= nend) {
+                if ((uint32_t)n >= R.ld(HW_NEND)) {
                     state = ST_IDLE;
                     break;
                 }
             }
             ++n;
-            again = start_sample(px, py);
+            again = start_sample(px, py, false);
             break;
         }
       }
@@ -1943,7 +1958,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                       rng.v3 = a.pix_states[3 * N + u];
                       rng.v4 = a.pix_states[4 * N + u];
                       rng.d = a.pix_states[5 * N + u];
-                      nend = a.pix_states[UW_NEND * N + u];
+                      R.st(HW_NEND, a.pix_states[UW_NEND * N + u]);
                       n = (int)(n0 & 0x7fffffffu);
                       const bool split = u >= a.nwhole;
                       fl = (n0 >> 31) ? CF_LENS : CF_CAMC;
@@ -1955,7 +1970,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                           fl |= (n == 1) ? CF_OWNER : CF_SHARE;
                       R.st4(HW_PXY, pxy, split ? a.pix_states[UW_TQ * N + u] : 0u, 0u, 0u);
                       R.st4(HW_M, 0u, 0u, 0u, 0u); R.st2(HW_M + 4, 0u, 0u);
-                      again = start_sample(pxy & 0xffffu, pxy >> 16);
+                      again = start_sample(pxy & 0xffffu, pxy >> 16, true);
                   }
               }
           }
@@ -1973,8 +1988,6 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     }
     SEC(SEC_RECORD);
     R.st4(HW_N, (uint32_t)n, stage, fl, rng.d);
-    R.st4(HW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
-    R.st4(HW_RNG_V4, rng.v4, nend, __float_as_uint(cu1), __float_as_uint(cu2));
 }
 
 // The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
@@ -2409,7 +2422,7 @@ struct pt_ctx {
     uint32_t wf_iters = 2;          // (PT_WF_ITERS)
     uint32_t wf_top = kTopNodesMax; // BVH4 nodes staged in each block's LDS (PT_WF_TOP; 0 = none)
     bool head_wf = true;            // integrator 1 on the wavefront kernel (PT_HEAD_WF=0: the tile kernel)
-    int head_min_waves = 4;         // its register budget (PT_HEAD_MIN_WAVES: 4 = 128 VGPRs, 5 = 96; 4 measured faster)
+    int head_min_waves = 5;         // its register budget (PT_HEAD_MIN_WAVES: 4 = 128 VGPRs, 5 = 96)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
@@ -3038,10 +3051,17 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         b.node_mask = c->node4_mask;
         b.top_nodes = c->top_nodes;
         b.head = head ? 1u : 0u;
-        const size_t lds_wf = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
-                              kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0) +
-                              (size_t)b.top_nodes * kTopNodeBytes;
         const uint32_t wpc = (head && !count) ? 4u * (uint32_t)c->head_min_waves : c->wf_waves_per_cu;
+        const size_t lds_fixed = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
+                                 kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0);
+        {   // as many top nodes as leave every block of a CU its LDS (granted in 1280-B granules): integrator 1's
+            // staged light normals cost it one node at 5 blocks per CU (97 -> 96), which kept it at 4 blocks
+            const uint32_t bpc = std::max(1u, wpc / 4u);
+            const size_t per_block = (size_t)(163840u / bpc) / 1280u * 1280u;
+            const uint32_t cap = per_block > lds_fixed ? (uint32_t)((per_block - lds_fixed) / kTopNodeBytes) : 1u;
+            if (b.top_nodes > 0) b.top_nodes = std::max(1u, std::min(b.top_nodes, cap));   // (0: no triangles, no BVH4)
+        }
+        const size_t lds_wf = lds_fixed + (size_t)b.top_nodes * kTopNodeBytes;
         uint32_t blocks = (uint32_t)c->num_cus * (wpc / 4 ? wpc / 4 : 1);
         // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
         // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`

@@ -483,5 +483,9 @@ def test_async_renders_queue_back_to_back(cb):
         r.wait()
     assert np.array_equal(a.cpu().numpy().view(np.uint32), ref0.view(np.uint32))
     assert np.array_equal(b.cpu().numpy().view(np.uint32), ref1.view(np.uint32))
-    for k in ("samples", "rays_traced", "rays_reference", "work_units"):
+    for k in ("samples", "rays_reference", "work_units"):
         assert sa[k] == st0[k] and sb[k] == st1[k]
+    # traced rays may differ by a few: a split pixel's later chunk traces its primary ray itself when
+    # the pixel's chunk 0 has not yet published it (a race of timing, not of results)
+    for x, y in ((sa, st0), (sb, st1)):
+        assert 0 < x["rays_traced"] <= x["rays_reference"] and abs(x["rays_traced"] - y["rays_traced"]) <= x["samples"]

@@ -286,12 +286,28 @@ int main(int argc, char** argv)
     }
     printf("scene tris %u, primary rays %zu, bounce rays %zu, LDS top budget %.0f B\n", sc.num_tris, prim.size(),
            bounce.size(), top_bytes);
-    const struct { int W; uint32_t max_tris; double node_bytes; } cfgs[] = {
-        {4, 8, 112}, {6, 12, 176}, {8, 16, 224}, {8, 8, 224}};
+    // quant: child planes as 8-bit steps of a power-of-two grid from the node's lower corner,
+    // rounded outward (a compressed node of one 128-B line: origin, exponents, 48 plane bytes,
+    // 8 child words)
+    const struct { int W; uint32_t max_tris; double node_bytes; bool quant; } cfgs[] = {
+        {4, 8, 112, false}, {4, 8, 64, true}, {6, 12, 176, false}, {8, 16, 224, false}, {8, 8, 224, false},
+        {8, 16, 112, true}};
     for (const auto& cf : cfgs) {
         Collapse col{bin, cf.W, cf.max_tris, {}};
         col.run(0, 0);
         std::vector<WNode> nodes = reorder_bfs(col.out);
+        if (cf.quant)
+            for (WNode& nd : nodes)
+                for (int ax = 0; ax < 3; ++ax) {
+                    float lo = INFINITY, hi = -INFINITY;
+                    for (int k = 0; k < nd.n; ++k) { lo = std::min(lo, nd.box[k][ax]); hi = std::max(hi, nd.box[k][3 + ax]); }
+                    const float step = std::ldexp(1.0f, (int)std::ceil(std::log2(std::max((hi - lo) / 255.0f, 1e-30f))));
+                    for (int k = 0; k < nd.n; ++k) {
+                        const float ql = std::floor((nd.box[k][ax] - lo) / step), qh = std::ceil((nd.box[k][3 + ax] - lo) / step);
+                        nd.box[k][ax] = lo + ql * step;
+                        nd.box[k][3 + ax] = lo + std::min(qh, 255.0f) * step;
+                    }
+                }
         const uint32_t ntop = (uint32_t)std::min<double>(nodes.size(), top_bytes / cf.node_bytes);
         Walker w{nodes, tris, ntop};
         int maxd = 0;
@@ -300,9 +316,9 @@ int main(int argc, char** argv)
         for (int set = 0; set < 2; ++set) {
             Stats st;
             for (const Ray& r : set ? bounce : prim) w.walk(r.o, r.d, st);
-            printf("W=%d maxtris=%2u nodes %7zu fill %.2f depth %2d top %3u | %s: steps %.2f visits %.2f (global %.2f) "
+            printf("W=%d%s maxtris=%2u nodes %7zu fill %.2f depth %2d top %3u | %s: steps %.2f visits %.2f (global %.2f) "
                    "tris %.2f leaf-only steps %.2f entered/visit %.2f\n",
-                   cf.W, cf.max_tris, nodes.size(), fill / nodes.size(), maxd, ntop, set ? "bounce " : "primary",
+                   cf.W, cf.quant ? "q" : " ", cf.max_tris, nodes.size(), fill / nodes.size(), maxd, ntop, set ? "bounce " : "primary",
                    st.steps / st.rays, st.visits / st.rays, (st.visits - st.top_visits) / st.rays, st.tris / st.rays,
                    st.leaf_only_steps / st.rays, st.entered / std::max(1.0, st.visits));
         }
