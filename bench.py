@@ -213,29 +213,32 @@ class FrameLoop:
     frame's stats: frame k+1 is queued before frame k's stats are collected, so the GPU never idles
     between frames (the host's return path and the next launches overlap the render).
     reduce(buf) -> work with .wait(), or None (one process, or a synchronous reduce).
+    streams: optional, one (torch) stream per framebuffer: frame k's zeroing, render and reduce are issued
+    on streams[k % len] (the current stream while they are issued), so consecutive frames are ordered
+    only by their own dependencies -- the next frame's seeding pre-pass and render blocks start while
+    this frame's render drains its last waves, and its split-pixel finalisation runs beside them.
     step() returns a frame's stats (the previous frame's when asynchronous, None for the first);
     `drain()` returns (the last frame's buffer once its reduce is ordered before whatever the caller
     does next, the stats of the frames still in flight)."""
 
-    def __init__(self, bufs, render, reduce=None, wait=None):
+    def __init__(self, bufs, render, reduce=None, wait=None, streams=None):
         self.bufs = list(bufs)
         self.render = render
         self.reduce = reduce
         self.wait = wait
+        self.streams = list(streams) if streams else None
         self.pending = [None] * len(self.bufs)
         self.frames = 0
         self.inflight = 0
 
     def step(self):
         k = self.frames % len(self.bufs)
-        if self.pending[k] is not None:
-            self.pending[k].wait()
-            self.pending[k] = None
-        buf = self.bufs[k]
-        buf.zero_()
-        st = self.render(buf)
-        if self.reduce is not None:
-            self.pending[k] = self.reduce(buf)
+        if self.streams:
+            import torch
+            with torch.cuda.stream(self.streams[k % len(self.streams)]):
+                st = self._issue(k)
+        else:
+            st = self._issue(k)
         self.frames += 1
         if self.wait is None:
             return st
@@ -244,6 +247,17 @@ class FrameLoop:
             self.inflight -= 1
             return self.wait()
         return None
+
+    def _issue(self, k):
+        if self.pending[k] is not None:
+            self.pending[k].wait()
+            self.pending[k] = None
+        buf = self.bufs[k]
+        buf.zero_()
+        st = self.render(buf)
+        if self.reduce is not None:
+            self.pending[k] = self.reduce(buf)
+        return st
 
     def drain(self):
         stats = []
@@ -299,6 +313,8 @@ def main():
                     help="diagnostic, single process only: render shard 0 of N (one GPU's share at N GPUs)")
     ap.add_argument("--sync-frames", action="store_true",
                     help="one blocking render per frame (pt_render_device) instead of frames queued back to back")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="frames queued back to back on one stream (no overlap of consecutive frames)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
@@ -339,22 +355,27 @@ def main():
     W, H = args.width, args.height
     cam = pt.make_camera(width=W, height=H, **cam_kw)
     r = pt.Renderer(scene, device=local)
-    # two framebuffers: frame k's RCCL reduce runs while frame k+1 renders into the other one
-    fbs = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(2 if distributed else 1)]
-    stream = torch.cuda.current_stream().cuda_stream
+    # two framebuffers (and, for frames queued back to back, two streams): frame k's RCCL reduce runs
+    # while frame k+1 renders into the other one
+    overlap = not args.sync_frames and not args.one_stream
+    fbs = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(2 if (distributed or overlap) else 1)]
 
     def render(buf, flags=0):
         return r.render_device(cam, buf.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
-                               flags=args.flags | flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
+                               flags=args.flags | flags, shard_index=rank, shard_count=shards,
+                               stream_ptr=torch.cuda.current_stream().cuda_stream)
 
     def render_async(buf):
         r.render_device_async(cam, buf.data_ptr(), W, H, args.spp, bounces=args.bounces, integrator=args.integrator,
-                              flags=args.flags, shard_index=rank, shard_count=shards, stream_ptr=stream)
+                              flags=args.flags, shard_index=rank, shard_count=shards,
+                              stream_ptr=torch.cuda.current_stream().cuda_stream)
 
+    red = make_reduce(dist, backend, rank) if distributed else None
     if args.sync_frames:
-        loop = FrameLoop(fbs, render, make_reduce(dist, backend, rank) if distributed else None)
+        loop = FrameLoop(fbs, render, red)
     else:
-        loop = FrameLoop(fbs, render_async, make_reduce(dist, backend, rank) if distributed else None, wait=r.wait)
+        loop = FrameLoop(fbs, render_async, red, wait=r.wait,
+                         streams=[torch.cuda.Stream() for _ in fbs] if overlap else None)
 
     # counting pass (same inputs, counting variant): algorithmic bytes of the render kernel
     counts = None

@@ -68,7 +68,7 @@ struct Args {
     uint32_t unit_queues;           // wavefront kernel: units dealt from kQueues counters (> 1) or one
     uint32_t tile_fast4;            // tile kernel: trace with the render-path BVH4 walk (winner check, exact
                                     // slow walk as fallback) instead of the reference-BVH culled walk
-    const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
+    const DNodeW* nodes4;           // render-path BVH4 (collapsed SAH BVH; 8 wide in PT_WIDE8 builds)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
     const RNode* wbox;              // per render-path slot: its triangle's reference parent node (left/right
@@ -2366,11 +2366,9 @@ struct pt_ctx {
     uint32_t* jump = nullptr;
     float4* shade_m = nullptr;        // merged shading records (Args::shade_m), or none
     uint32_t* jump_bytes = nullptr;   // byte-position jump matrices (built on the first wavefront render)
-    uint32_t* seed_states = nullptr;  // per-render seed_table output
+    hipEvent_t jump_ready = nullptr;  // recorded behind their build
     bool use_jump_bytes = true;       // PT_JUMP_BYTES=0: per-bit jumps only
     bool tile_fast4 = true;           // PT_TILE_FAST4=0: the tile kernel walks the reference BVH (culled)
-    unsigned long long* counters = nullptr;
-    uint32_t* tile_counter = nullptr;
     float* scratch_out = nullptr;
     size_t scratch_bytes = 0;
     uint32_t num_lights = 0;
@@ -2394,11 +2392,27 @@ struct pt_ctx {
     };
     static constexpr int kFlights = 2;
     Flight fl[kFlights];
+    // A render's device scratch, one set per in-flight slot, so that two queued renders (e.g. frames on
+    // two streams) never share a buffer; set 0 also serves the batched trace entry points.
+    struct Bufs {
+        uint32_t* spill = nullptr;            // per-lane stack spill columns, then the shading records
+        size_t spill_words = 0;
+        uint32_t* pix_states = nullptr;       // init_pixel_states output (kUnitWords per work unit)
+        size_t pix_states_words = 0;
+        double* lbuf = nullptr;               // per-sample radiance of split pixels
+        size_t lbuf_words = 0;
+        uint32_t* pmemo = nullptr;            // per-pixel-slot primary hit shared by a split pixel's chunks
+        size_t pmemo_words = 0;
+        unsigned long long* counters = nullptr;
+        uint32_t* pixel_counter = nullptr;    // the unit queues
+        uint32_t* tile_counter = nullptr;
+        uint32_t* seed_states = nullptr;      // per-render seed_table output
+        uint64_t seed_cached = 0;             // the seed seed_states was built for
+        bool seed_valid = false;
+    };
+    Bufs rb[kFlights];
     int fl_head = 0, fl_n = 0;                 // oldest in-flight slot, number in flight
-    uint64_t seed_cached = 0;                  // the seed seed_states was built for
-    bool seed_valid = false;
     int num_cus = 256;
-    uint32_t* pixel_counter = nullptr;
     bool scene_fast = false;
     uint32_t node_mask = 0;
     uint32_t wf_threshold = 56;     // measured best at 5 waves/SIMD (C3: 24..64 swept)
@@ -2424,18 +2438,10 @@ struct pt_ctx {
     bool head_wf = true;            // integrator 1 on the wavefront kernel (PT_HEAD_WF=0: the tile kernel)
     int head_min_waves = 5;         // its register budget (PT_HEAD_MIN_WAVES: 4 = 128 VGPRs, 5 = 96)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
-    DNode4* nodes4 = nullptr;
+    DNodeW* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
     RNode* wbox = nullptr;
-    uint32_t* spill = nullptr;
-    size_t spill_words = 0;
-    uint32_t* pix_states = nullptr;   // init_pixel_states output (kUnitWords per work unit)
-    size_t pix_states_words = 0;
-    double* lbuf = nullptr;           // per-sample radiance of split pixels
-    size_t lbuf_words = 0;
-    uint32_t* pmemo = nullptr;        // per-pixel-slot primary hit shared by a split pixel's chunks
-    size_t pmemo_words = 0;
     float* tone_thr = nullptr;        // output step: the host libm's 255 code boundaries (+ t[0] = 0)
     bool tone_ok = false;
     float4* spheres = nullptr;        // sphere primitives (center, radius)
@@ -2454,7 +2460,8 @@ int pt::ctx_device(const pt_ctx* c) { return c->device; }
 // Per-lane HBM words the walks may need: the BVH4 ring's overflow (at most 3 pushes per level)
 // and trace_slow's full stack on the reference BVH.
 static size_t stack_words_per_lane(const pt_ctx* c);
-static int ensure_spill(pt_ctx* c, size_t words);
+static int ensure_spill(pt_ctx::Bufs& B, size_t words);
+static bool alloc_bufs(pt_ctx::Bufs& B);
 
 extern "C" {
 
@@ -2659,7 +2666,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
     }
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
-    std::vector<DNode4> an;
+    std::vector<DNodeW> an;
     std::vector<DTri> at;
     if (nt == 0) {   // spheres only: no triangle structures (kernels skip the walk)
         for (int q = 0; q < 3; ++q) { c->acc_root[q] = INFINITY; c->acc_root[3 + q] = -INFINITY; }
@@ -2667,12 +2674,22 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->node4_mask = 1u;
     } else {
         pt::AccelBvh acc;
+#ifdef PT_WIDE8
+        constexpr int kW = 8;
+        pt::Accel8 acc4;
+#else
+        constexpr int kW = 4;
         pt::Accel4 acc4;
+#endif
         lap("reference-BVH records");
         int rc4 = pt::build_accel(*sc, &acc);
         lap("SAH BVH build");
         if (timing && rc4 == PT_OK) fprintf(stderr, "pt_create: render BVH SAH cost %.6g\n", pt::accel_sah_cost(acc));
+#ifdef PT_WIDE8
+        if (rc4 == PT_OK) rc4 = pt::collapse_accel8(acc, &acc4);
+#else
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
+#endif
         lap("BVH4 collapse");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }
         // Node order: the kTopNodesMax nodes most likely to be visited first (best-first by box
@@ -2689,8 +2706,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                 heap.pop_back();
                 new_of[o] = (uint32_t)old_of.size();
                 old_of.push_back(o);
-                const pt::Accel4Node& x = acc4.nodes[o];
-                for (int k = 0; k < 4; ++k) {
+                const auto& x = acc4.nodes[o];
+                for (int k = 0; k < kW; ++k) {
                     if (x.child[k] == pt::kAccel4Empty || (x.child[k] & PT_BVH_LEAF_FLAG)) continue;
                     const float b[6] = {x.lo[0][k], x.lo[1][k], x.lo[2][k], x.hi[0][k], x.hi[1][k], x.hi[2][k]};
                     const float ex = b[3] - b[0], ey = b[4] - b[1], ez = b[5] - b[2];
@@ -2711,20 +2728,20 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         std::vector<uint32_t> slot_leaf;
         slot_leaf.reserve(nt);
         for (size_t i = 0; i < n4; ++i) {
-            pt::Accel4Node x0 = acc4.nodes[old_of[i]], x = x0;
+            auto x0 = acc4.nodes[old_of[i]], x = x0;
             auto is_leaf = [](uint32_t r) { return r != pt::kAccel4Empty && (r & PT_BVH_LEAF_FLAG); };
-            int order[4], m = 0;
-            for (int k = 0; k < 4; ++k) if (is_leaf(x0.child[k])) order[m++] = k;
-            for (int k = 0; k < 4; ++k) if (!is_leaf(x0.child[k])) order[m++] = k;
+            int order[kW], m = 0;
+            for (int k = 0; k < kW; ++k) if (is_leaf(x0.child[k])) order[m++] = k;
+            for (int k = 0; k < kW; ++k) if (!is_leaf(x0.child[k])) order[m++] = k;
             const uint32_t base = (uint32_t)slot_leaf.size();
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < kW; ++k) {
                 const int q = order[k];
                 for (int ax = 0; ax < 3; ++ax) { x.lo[ax][k] = x0.lo[ax][q]; x.hi[ax][k] = x0.hi[ax][q]; }
                 x.child[k] = x0.child[q];
                 if (is_leaf(x.child[k])) {
                     const uint32_t first = (uint32_t)slot_leaf.size() - base, cnt = pt::accel_leaf_count(x.child[k]);
                     for (uint32_t j = 0; j < cnt; ++j) slot_leaf.push_back(pt::accel_leaf_slot(x.child[k]) + j);
-                    static_assert(pt::kAccel4LeafTris <= kLeafBits, "leaf slot mask width");
+                    static_assert(pt::kAccel4LeafTris <= kLeafBits && pt::kAccel8LeafTris <= kLeafBits, "leaf slot mask width");
                     if (first + cnt > kLeafBits || base >= (1u << (31 - kLeafBits))) {
                         delete c;
                         return bail(pt::fail(PT_E_SCENE, "pt_create: %u triangles exceed the render path's leaf slot range", nt));
@@ -2732,8 +2749,51 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                     x.child[k] = PT_BVH_LEAF_FLAG | (base << kLeafBits) | (((1u << cnt) - 1u) << first);
                 }
             }
-            for (int k = 0; k < 4; ++k)
+            for (int k = 0; k < kW; ++k)
                 if (x.child[k] != pt::kAccel4Empty && !(x.child[k] & PT_BVH_LEAF_FLAG)) x.child[k] = new_of[x.child[k]];
+#ifdef PT_WIDE8
+            {   // quantize: per axis the origin (lowest child plane) and the least power-of-two step with
+                // 255 steps >= the extent; planes rounded outward to the grid; empty slots inverted
+                uint32_t q[3][2][8];
+                float org[3];
+                uint32_t ebytes = 0;
+                for (int ax = 0; ax < 3; ++ax) {
+                    float lo = INFINITY, hi = -INFINITY;
+                    for (int k = 0; k < kW; ++k)
+                        if (x.child[k] != pt::kAccel4Empty) { lo = std::fmin(lo, x.lo[ax][k]); hi = std::fmax(hi, x.hi[ax][k]); }
+                    const double ext = (double)hi - (double)lo;
+                    int e = -60;
+                    if (ext > 0.0) e = std::max(-60, (int)std::ceil(std::log2(ext / 255.0)));
+                    while (std::ldexp(255.0, e) < ext) ++e;
+                    org[ax] = lo;
+                    ebytes |= (uint32_t)(e + 128) << (8 * ax);
+                    for (int k = 0; k < kW; ++k) {
+                        if (x.child[k] == pt::kAccel4Empty) { q[ax][0][k] = 255u; q[ax][1][k] = 0u; continue; }
+                        const double a = std::floor(std::ldexp((double)x.lo[ax][k] - (double)lo, -e));
+                        const double b = std::ceil(std::ldexp((double)x.hi[ax][k] - (double)lo, -e));
+                        if (!(a >= 0.0 && b <= 255.0 && a <= b)) {
+                            delete c;
+                            return bail(pt::fail(PT_E_SCENE, "pt_create: 8-wide node quantization out of range"));
+                        }
+                        q[ax][0][k] = (uint32_t)a;
+                        q[ax][1][k] = (uint32_t)b;
+                    }
+                }
+                auto pack4 = [](const uint32_t* b) { return b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24; };
+                float ebf;
+                memcpy(&ebf, &ebytes, 4);
+                an[i].hdr = make_float4(org[0], org[1], org[2], ebf);
+                uint4* qa[3] = {&an[i].qx, &an[i].qy, &an[i].qz};
+                for (int ax = 0; ax < 3; ++ax)
+                    *qa[ax] = make_uint4(pack4(q[ax][0]), pack4(q[ax][0] + 4), pack4(q[ax][1]), pack4(q[ax][1] + 4));
+                uint32_t cw[kW];
+                for (int k = 0; k < kW; ++k)   // an empty slot's word: a leaf of empty mask at the node's base
+                    cw[k] = (x.child[k] == pt::kAccel4Empty) ? (PT_BVH_LEAF_FLAG | (base << kLeafBits)) : x.child[k];
+                an[i].c0 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+                an[i].c1 = make_uint4(cw[4], cw[5], cw[6], cw[7]);
+                an[i].pad[0] = an[i].pad[1] = make_uint4(0u, 0u, 0u, 0u);
+            }
+#else
             an[i].lox = make_float4(x.lo[0][0], x.lo[0][1], x.lo[0][2], x.lo[0][3]);
             an[i].loy = make_float4(x.lo[1][0], x.lo[1][1], x.lo[1][2], x.lo[1][3]);
             an[i].loz = make_float4(x.lo[2][0], x.lo[2][1], x.lo[2][2], x.lo[2][3]);
@@ -2742,6 +2802,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             an[i].hiz = make_float4(x.hi[2][0], x.hi[2][1], x.hi[2][2], x.hi[2][3]);
             an[i].child = make_uint4(x.child[0], x.child[1], x.child[2], x.child[3]);
             an[i].pad = make_uint4(0u, 0u, 0u, 0u);
+#endif
         }
         if (slot_leaf.size() != nt) { delete c; return bail(pt::fail(PT_E_SCENE, "pt_create: BVH4 reaches %zu of %u triangles", slot_leaf.size(), nt)); }
         at.resize(nt);
@@ -2881,10 +2942,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         pt_destroy(c);
         return bail(rc);
     }
-    if (hipMalloc(reinterpret_cast<void**>(&c->counters), kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->tile_counter), 16) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->pixel_counter), kQueueStride * (kQueues + 1) * 4) != hipSuccess ||
-        !create_flights(c)) {
+    if (!alloc_bufs(c->rb[0]) || !create_flights(c)) {
         pt_destroy(c);
         return bail(pt::fail(PT_E_HIP, "pt_create: device allocation failed"));
     }
@@ -2898,12 +2956,17 @@ void pt_destroy(pt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
-                    c->lights, c->jump, c->jump_bytes, c->seed_states, c->shade_m, c->counters, c->tile_counter, c->scratch_out, c->pixel_counter,
-                    c->nodes4, c->acc_tris, c->rparent, c->wbox, c->spill, c->pix_states, c->lbuf, c->pmemo,
+                    c->lights, c->jump, c->jump_bytes, c->shade_m, c->scratch_out,
+                    c->nodes4, c->acc_tris, c->rparent, c->wbox,
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (pt_ctx::Bufs& B : c->rb)
+        for (void* b : {(void*)B.spill, (void*)B.pix_states, (void*)B.lbuf, (void*)B.pmemo, (void*)B.counters,
+                        (void*)B.pixel_counter, (void*)B.tile_counter, (void*)B.seed_states})
+            if (b) (void)hipFree(b);
     pt::free_pinned(c->pinned);
+    if (c->jump_ready) (void)hipEventDestroy(c->jump_ready);
     for (pt_ctx::Flight& f : c->fl) {
         for (hipEvent_t e : {f.ev0, f.ev1, f.ek0, f.ek1, f.done})
             if (e) (void)hipEventDestroy(e);
@@ -2966,12 +3029,19 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             return pt::fail(PT_E_INVALID, "pt_render: tile size %dx%d (0 = 8, else multiples of 8 up to 256)", p->tile_w, p->tile_h);
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+    // this render's slot: its events and its buffer set.  The slot's previous render was collected by
+    // pt_render_wait (its events synchronised), so two queued renders -- on one stream or on two, where
+    // they may run concurrently -- never share a buffer.
+    const int slot = (c->fl_head + c->fl_n) % pt_ctx::kFlights;
+    pt_ctx::Flight& F = c->fl[slot];
+    pt_ctx::Bufs& B = c->rb[slot];
+    if (!alloc_bufs(B)) return pt::fail(PT_E_HIP, "pt_render: device allocation failed");
 
     Args a;
     memset(&a, 0, sizeof(a));
     a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
     a.shade = c->shade; a.mats = c->mats; a.lights = c->lights; a.jump = c->jump; a.shade_m = c->shade_m;
-    a.out = d_out; a.counters = c->counters; a.tile_counter = c->tile_counter;
+    a.out = d_out; a.counters = B.counters; a.tile_counter = B.tile_counter;
     a.num_lights = c->num_lights; a.total_light_area = c->total_light_area;
     a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;
     a.sphere_mat_base = c->sphere_mat_base;
@@ -2999,7 +3069,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     const size_t lds = (size_t)a.stack_words * 4;
     if (lds > 160 * 1024) return pt::fail(PT_E_BVH_DEPTH, "pt_render: BVH depth %d needs %zu B of LDS stack", c->depth, lds);
 
-    a.pixel_counter = c->pixel_counter;
+    a.pixel_counter = B.pixel_counter;
     a.nunits = a.ntiles_shard * tw * th;
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.wf_threshold = c->wf_threshold;
@@ -3020,15 +3090,13 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     const bool wavefront = (p->integrator == PT_INTEGRATOR_UNIDIR || (head && c->head_wf)) && !refwalk &&
                            !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam &&
                            p->width < 65536 && p->height < 65536;   // (16-bit pixel coordinates per unit)
-    pt_ctx::Flight& F = c->fl[(c->fl_head + c->fl_n) % pt_ctx::kFlights];
-    if (c->fl_n > 0)   // (a render in flight on another stream still uses the context's buffers)
-        HIP_TRY(hipStreamWaitEvent(stream, c->fl[(c->fl_head + c->fl_n - 1) % pt_ctx::kFlights].done, 0));
+
     // (the wavefront path's init_pixel_states resets the counters itself: one launch less per frame)
     if (!(p->spp > 0 && a.ntiles_shard > 0 && wavefront)) {
-        HIP_TRY(hipMemsetAsync(c->counters, 0, kCounterWords * sizeof(unsigned long long), stream));
-        HIP_TRY(hipMemsetAsync(c->counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
-        HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, stream));
-        HIP_TRY(hipMemsetAsync(c->pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
+        HIP_TRY(hipMemsetAsync(B.counters, 0, kCounterWords * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(B.counters + 20, 0xff, 2 * sizeof(unsigned long long), stream));   // (atomicMin slots)
+        HIP_TRY(hipMemsetAsync(B.tile_counter, 0, 16, stream));
+        HIP_TRY(hipMemsetAsync(B.pixel_counter, 0, kQueueStride * (kQueues + 1) * 4, stream));
     }
     if (count && (p->flags & PT_FLAG_TRI_COUNTS)) {   // per-triangle test counts of this render (pt_tri_counts)
         HIP_TRY(hipMemsetAsync(c->tri_counts, 0, (size_t)std::max<uint32_t>(c->num_tris, 1u) * 4, stream));
@@ -3114,7 +3182,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             } else {
                 size_t fr = 0, tot = 0;
                 HIP_TRY(hipMemGetInfo(&fr, &tot));
-                budget = ((uint64_t)fr + (uint64_t)c->lbuf_words * sizeof(double)) / 4;
+                budget = ((uint64_t)fr + (uint64_t)B.lbuf_words * sizeof(double)) / 4;
             }
             const uint64_t cap = budget / ((uint64_t)p->spp * 3 * sizeof(double));
             if (ntail > cap) {
@@ -3147,41 +3215,41 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         if (blocks > need) blocks = need;
         if (ntail > 0) {
             const size_t lw = (size_t)ntail * (size_t)p->spp * 3;
-            if (c->lbuf_words < lw) {
-                if (c->lbuf) (void)hipFree(c->lbuf);
-                c->lbuf = nullptr;
-                c->lbuf_words = 0;
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->lbuf), lw * sizeof(double)));
-                c->lbuf_words = lw;
+            if (B.lbuf_words < lw) {
+                if (B.lbuf) (void)hipFree(B.lbuf);
+                B.lbuf = nullptr;
+                B.lbuf_words = 0;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&B.lbuf), lw * sizeof(double)));
+                B.lbuf_words = lw;
             }
-            b.lbuf = c->lbuf;
+            b.lbuf = B.lbuf;
             const size_t mw = (size_t)ntail * 2;
-            if (c->pmemo_words < mw) {
-                if (c->pmemo) (void)hipFree(c->pmemo);
-                c->pmemo = nullptr;
-                c->pmemo_words = 0;
-                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pmemo), mw * 4));
-                c->pmemo_words = mw;
+            if (B.pmemo_words < mw) {
+                if (B.pmemo) (void)hipFree(B.pmemo);
+                B.pmemo = nullptr;
+                B.pmemo_words = 0;
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&B.pmemo), mw * 4));
+                B.pmemo_words = mw;
             }
-            b.pmemo = c->pmemo;
+            b.pmemo = B.pmemo;
         }
         const size_t per_lane = stack_words_per_lane(c);
         const size_t rec_words = head ? (size_t)kHeadWords : (size_t)kColdWords;   // shading record per lane
-        if (int rc = ensure_spill(c, per_lane * (size_t)blocks * 256 + rec_words * (size_t)blocks * paths_per_block))
+        if (int rc = ensure_spill(B, per_lane * (size_t)blocks * 256 + rec_words * (size_t)blocks * paths_per_block))
             return rc;
-        b.spill = c->spill;
+        b.spill = B.spill;
         b.spill_stride = blocks * 256;
         b.cold_stride = blocks * paths_per_block;
-        b.cold = c->spill + per_lane * (size_t)b.spill_stride;
+        b.cold = B.spill + per_lane * (size_t)b.spill_stride;
         const size_t sw = (size_t)kUnitWords * b.nunits;
-        if (c->pix_states_words < sw) {
-            if (c->pix_states) (void)hipFree(c->pix_states);
-            c->pix_states = nullptr;
-            c->pix_states_words = 0;
-            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pix_states), sw * 4));
-            c->pix_states_words = sw;
+        if (B.pix_states_words < sw) {
+            if (B.pix_states) (void)hipFree(B.pix_states);
+            B.pix_states = nullptr;
+            B.pix_states_words = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&B.pix_states), sw * 4));
+            B.pix_states_words = sw;
         }
-        b.pix_states = c->pix_states;
+        b.pix_states = B.pix_states;
         // diagnostic: per-lane end / per-wave start and exit times (PT_LANE_TIMING=file appends a summary)
         const char* timing_path = getenv("PT_LANE_TIMING");
         std::vector<unsigned long long> times;
@@ -3196,27 +3264,32 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             if (!c->jump_bytes) {   // once per context: 512 byte-sliced 160x160 GF(2) matrices (84 MB)
                 // (built into locals and published only once the build launched: a failure leaves the
                 // context without tables, so the next render tries again instead of seeding from garbage)
-                uint32_t *jb = nullptr, *ss = nullptr;
+                // (a render queued on another stream meanwhile waits for the build: jump_ready)
+                uint32_t* jb = nullptr;
                 const bool ok = hipMalloc(reinterpret_cast<void**>(&jb), (size_t)512 * 20 * 256 * kJumpEntryWords * 4) == hipSuccess &&
-                                hipMalloc(reinterpret_cast<void**>(&ss), (size_t)256 * kJumpEntryWords * 4) == hipSuccess;
+                                (c->jump_ready || hipEventCreateWithFlags(&c->jump_ready, hipEventDisableTiming) == hipSuccess);
                 if (ok) hipLaunchKernelGGL(build_jump_byte_tables, dim3(512 * 20), dim3(256), 0, stream, c->jump, jb);
-                if (!ok || hipGetLastError() != hipSuccess) {
+                if (!ok || hipGetLastError() != hipSuccess || hipEventRecord(c->jump_ready, stream) != hipSuccess) {
                     if (jb) (void)hipFree(jb);
-                    if (ss) (void)hipFree(ss);
                     return pt::fail(ok ? PT_E_HIP : PT_E_OOM, "pt_render: jump-table setup failed");
                 }
                 c->jump_bytes = jb;
-                c->seed_states = ss;
+            } else {
+                HIP_TRY(hipStreamWaitEvent(stream, c->jump_ready, 0));
             }
-            if (!c->seed_valid || c->seed_cached != p->seed) {   // (depends on the seed only: kept across renders)
-                hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, c->seed_states);
-                c->seed_cached = p->seed;
-                c->seed_valid = true;
+            if (!B.seed_states) {
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&B.seed_states), (size_t)256 * kJumpEntryWords * 4));
+                B.seed_valid = false;
+            }
+            if (!B.seed_valid || B.seed_cached != p->seed) {   // (depends on the seed only: kept across renders)
+                hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, B.seed_states);
+                B.seed_cached = p->seed;
+                B.seed_valid = true;
             }
             b.jump_bytes = c->jump_bytes;
-            b.seed_states = c->seed_states;
+            b.seed_states = B.seed_states;
         }
-        hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, c->pix_states);
+        hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, B.pix_states);
         HIP_TRY(hipEventRecord(F.ek0, stream));
         kernel_events = true;
         units = b.nunits;
@@ -3243,8 +3316,8 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         }
     } else if (p->spp > 0 && a.ntiles_shard > 0) {
         if (a.tile_fast4) {   // the BVH4 walk's ring overflow and the slow walk's stack: one HBM column per lane
-            if (int rc = ensure_spill(c, stack_words_per_lane(c) * (size_t)grid * 64)) return rc;
-            a.spill = c->spill;
+            if (int rc = ensure_spill(B, stack_words_per_lane(c) * (size_t)grid * 64)) return rc;
+            a.spill = B.spill;
             a.spill_stride = grid * 64;
         }
 #define PT_LAUNCH(I, R, C) hipLaunchKernelGGL((render_tiles<I, R, C>), dim3(grid), dim3(64), lds, stream, a)
@@ -3259,7 +3332,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(F.ev1, stream));
-    HIP_TRY(hipMemcpyAsync(F.hcnt, c->counters, kCounterWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(F.hcnt, B.counters, kCounterWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipEventRecord(F.done, stream));
     F.kernel_events = kernel_events;
     F.count = count;
@@ -3408,20 +3481,32 @@ int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rg
 
 static size_t stack_words_per_lane(const pt_ctx* c)
 {
+#ifdef PT_WIDE8
+    size_t per_lane = (size_t)(7 * c->acc4_depth + 4);   // (an 8-wide visit pushes at most 7 entries)
+#else
     size_t per_lane = (size_t)(3 * c->acc4_depth + 4);
+#endif
     if (per_lane < (size_t)(2 * (c->depth + 2))) per_lane = (size_t)(2 * (c->depth + 2));
     return per_lane;
 }
 
-static int ensure_spill(pt_ctx* c, size_t words)
+static int ensure_spill(pt_ctx::Bufs& B, size_t words)
 {
-    if (c->spill_words >= words) return PT_OK;
-    if (c->spill) (void)hipFree(c->spill);
-    c->spill = nullptr;
-    c->spill_words = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->spill), words * 4));
-    c->spill_words = words;
+    if (B.spill_words >= words) return PT_OK;
+    if (B.spill) (void)hipFree(B.spill);
+    B.spill = nullptr;
+    B.spill_words = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&B.spill), words * 4));
+    B.spill_words = words;
     return PT_OK;
+}
+
+static bool alloc_bufs(pt_ctx::Bufs& B)
+{
+    if (B.counters) return true;
+    return hipMalloc(reinterpret_cast<void**>(&B.counters), kCounterWords * sizeof(unsigned long long)) == hipSuccess &&
+           hipMalloc(reinterpret_cast<void**>(&B.tile_counter), 16) == hipSuccess &&
+           hipMalloc(reinterpret_cast<void**>(&B.pixel_counter), kQueueStride * (kQueues + 1) * 4) == hipSuccess;
 }
 
 extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags)
@@ -3453,7 +3538,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
     Args a;
     memset(&a, 0, sizeof(a));
     a.nodes = c->nodes; a.rnodes = c->rnodes; a.tris_leaf = c->tris_leaf; a.tris_orig = c->tris_orig;
-    a.counters = c->counters;
+    a.counters = c->rb[0].counters;
     a.spheres = c->spheres; a.num_spheres = c->num_spheres; a.num_tris = c->num_tris;
     a.sphere_mat_base = c->sphere_mat_base;
     memcpy(a.root, c->root, sizeof(a.root));
@@ -3472,8 +3557,8 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
     uint32_t blocks = (n + 255) / 256;
     const uint32_t cap = (uint32_t)c->num_cus * 8u;
     if (blocks > cap) blocks = cap;
-    if (int rc = ensure_spill(c, stack_words_per_lane(c) * (size_t)blocks * 256)) return rc;
-    a.spill = c->spill;
+    if (int rc = ensure_spill(c->rb[0], stack_words_per_lane(c) * (size_t)blocks * 256)) return rc;
+    a.spill = c->rb[0].spill;
     a.spill_stride = blocks * 256;
     float* d_rays = nullptr;
     int32_t* d_tri = nullptr;
@@ -3485,7 +3570,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_tri), (size_t)n * 4));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_t), (size_t)n * 4));
         HIP_TRY(hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemset(c->counters, 0, kCounterWords * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(c->rb[0].counters, 0, kCounterWords * sizeof(unsigned long long)));
         const bool count = tri_counts != nullptr || spill_entries != nullptr;
         if (tri_counts && c->num_tris > 0) {   // (own scratch: the last render's counts stay for pt_tri_counts)
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d_cnt), (size_t)c->num_tris * 4));
@@ -3507,7 +3592,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
         }
         if (spill_entries) {
             unsigned long long v = 0;
-            HIP_TRY(hipMemcpy(&v, c->counters + 25, sizeof(v), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(&v, c->rb[0].counters + 25, sizeof(v), hipMemcpyDeviceToHost));
             *spill_entries = v;
         }
         return PT_OK;

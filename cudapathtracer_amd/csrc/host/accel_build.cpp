@@ -318,33 +318,35 @@ float area_of(const float* b)
     return surface(b, b + 3);
 }
 
+// W-wide collapse (W = 4: Accel4; W = 8: Accel8), at most kTris triangles in a node's leaf children
+template <int W, uint32_t kTris, class Node, class Out>
 struct Collapser {
     const AccelBvh& bin;
-    Accel4& out;
+    Out& out;
     int max_depth = 0;
 
-    // Collapse the subtree whose binary root is inner node `b`; returns its 4-wide index.
+    // Collapse the subtree whose binary root is inner node `b`; returns its W-wide index.
     uint32_t run(uint32_t b, int depth)
     {
         max_depth = std::max(max_depth, depth);
         struct Cand { uint32_t ref; float box[6]; };
-        Cand c[4];
+        Cand c[W];
         int n = 2;
         for (int k = 0; k < 2; ++k) {
             c[k].ref = bin.nodes[b].child[k];
             memcpy(c[k].box, bin.nodes[b].box[k], sizeof(c[k].box));
         }
         // triangles in the leaf children (the walk queues a node's entered leaf triangles as one
-        // entry with a kAccel4LeafTris-bit slot mask)
+        // entry with a kTris-bit slot mask)
         auto leaf_tris = [](uint32_t ref) { return (ref & PT_BVH_LEAF_FLAG) ? accel_leaf_count(ref) : 0u; };
         uint32_t tris = leaf_tris(c[0].ref) + leaf_tris(c[1].ref);
-        while (n < 4) {   // expand the inner candidate with the largest surface area
+        while (n < W) {   // expand the inner candidate with the largest surface area
             int pick = -1;
             float best = -1.0f;
             for (int k = 0; k < n; ++k) {
                 if (c[k].ref & PT_BVH_LEAF_FLAG) continue;
                 const AccelNode& y = bin.nodes[c[k].ref];
-                if (tris + leaf_tris(y.child[0]) + leaf_tris(y.child[1]) > kAccel4LeafTris) continue;
+                if (tris + leaf_tris(y.child[0]) + leaf_tris(y.child[1]) > kTris) continue;
                 const float a = area_of(c[k].box);
                 if (a > best) { best = a; pick = k; }
             }
@@ -360,13 +362,13 @@ struct Collapser {
         }
         const uint32_t me = static_cast<uint32_t>(out.nodes.size());
         out.nodes.emplace_back();
-        uint32_t refs[4];
-        for (int k = 0; k < 4; ++k) {
+        uint32_t refs[W];
+        for (int k = 0; k < W; ++k) {
             if (k >= n) { refs[k] = kAccel4Empty; continue; }
             refs[k] = (c[k].ref & PT_BVH_LEAF_FLAG) ? c[k].ref : run(c[k].ref, depth + 1);
         }
-        Accel4Node& nd = out.nodes[me];
-        for (int k = 0; k < 4; ++k) {
+        Node& nd = out.nodes[me];
+        for (int k = 0; k < W; ++k) {
             for (int ax = 0; ax < 3; ++ax) {
                 // empty slot: a point at 2^100 -- every ray rejects it (entry >= 2^99 beyond any
                 // best distance, or exit behind the origin; o*inv stays finite, so no NaN), which
@@ -386,9 +388,20 @@ int collapse_accel4(const AccelBvh& bin, Accel4* out)
 {
     out->nodes.clear();
     out->nodes.reserve(bin.nodes.size() / 2 + 1);
-    Collapser col{bin, *out};
+    Collapser<4, kAccel4LeafTris, Accel4Node, Accel4> col{bin, *out};
     const uint32_t root = col.run(0, 0);
     if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
+    out->depth = col.max_depth;
+    return PT_OK;
+}
+
+int collapse_accel8(const AccelBvh& bin, Accel8* out)
+{
+    out->nodes.clear();
+    out->nodes.reserve(bin.nodes.size() / 3 + 1);
+    Collapser<8, kAccel8LeafTris, Accel8Node, Accel8> col{bin, *out};
+    const uint32_t root = col.run(0, 0);
+    if (root != 0) return fail(PT_E_SCENE, "collapse_accel8: internal error");
     out->depth = col.max_depth;
     return PT_OK;
 }

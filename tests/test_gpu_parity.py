@@ -489,3 +489,41 @@ def test_async_renders_queue_back_to_back(cb):
     # the pixel's chunk 0 has not yet published it (a race of timing, not of results)
     for x, y in ((sa, st0), (sb, st1)):
         assert 0 < x["rays_traced"] <= x["rays_reference"] and abs(x["rays_traced"] - y["rays_traced"]) <= x["samples"]
+
+
+@pytest.mark.gpu
+def test_async_renders_on_two_streams(cb):
+    """Two renders queued on two streams (frames that may run concurrently: each in-flight slot has its own
+    scratch -- records, unit table, split-pixel samples, memo words, queues, seed table), repeated so that
+    both slots are reused: every image and count equals the blocking render's."""
+    import torch
+    s, r = cb
+    w, h, spp = 96, 64, 6
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    cases = [dict(shard_index=0, shard_count=3), dict(shard_index=2, shard_count=3, integrator=1),
+             dict(shard_index=1, shard_count=3)]
+    refs = [r.render(cam, w, h, spp, bounces=3, **kw) for kw in cases]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = [torch.zeros((h, w, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
+    got = []
+    for rep in range(2):
+        for k, kw in enumerate(cases):
+            st = streams[k % 2]
+            with torch.cuda.stream(st):
+                bufs[k % 2].zero_()
+                r.render_device_async(cam, bufs[k % 2].data_ptr(), w, h, spp, bounces=3, stream_ptr=st.cuda_stream, **kw)
+            if k % 2 == 1 or k == len(cases) - 1:   # collect after both slots were queued
+                while True:
+                    try:
+                        got.append(r.wait())
+                    except pt.PtError:
+                        break
+                torch.cuda.synchronize()
+                for j in range(k - (1 if k % 2 == 1 else 0), k + 1):
+                    img = bufs[j % 2].cpu().numpy()
+                    assert np.array_equal(img.view(np.uint32), refs[j][0].view(np.uint32)), (rep, j)
+    assert len(got) == 2 * len(cases)
+    for j, st in enumerate(got):
+        ref = refs[j % len(cases)][1]
+        for key in ("samples", "rays_reference", "work_units", "split_pixels"):
+            assert st[key] == ref[key], (j, key)
