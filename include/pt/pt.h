@@ -231,11 +231,11 @@ int pt_render_device(pt_ctx* ctx, const pt_params* params, const pt_camera* cam,
                      void* stream, pt_stats* stats);
 
 /* pt_render_device in two halves: _async enqueues the whole render on `stream` and returns at once (up
- * to 2 renders in flight per context; a second one on another stream is ordered behind the first, since
- * they share the context's work buffers); pt_render_wait waits for the OLDEST render in flight and
- * returns its stats.  Frames queued back to back leave the GPU no idle gap between them (the bench's
- * frame loop).  pt_render_device = _async + wait, and refuses to run while renders are in flight, as
- * do pt_trace* and pt_tri_counts. */
+ * to 2 renders in flight per context, each with its own work buffers: two renders on two streams may run
+ * concurrently -- the next frame's blocks start while this one's last waves drain); pt_render_wait waits
+ * for the OLDEST render in flight and returns its stats.  Frames queued back to back leave the GPU no
+ * idle gap between them (the bench's frame loop).  pt_render_device = _async + wait, and refuses to run
+ * while renders are in flight, as do pt_trace* and pt_tri_counts. */
 int pt_render_device_async(pt_ctx* ctx, const pt_params* params, const pt_camera* cam, float* d_out, void* stream);
 int pt_render_wait(pt_ctx* ctx, pt_stats* stats);
 
