@@ -314,7 +314,9 @@ def main():
     ap.add_argument("--sync-frames", action="store_true",
                     help="one blocking render per frame (pt_render_device) instead of frames queued back to back")
     ap.add_argument("--one-stream", action="store_true",
-                    help="frames queued back to back on one stream (no overlap of consecutive frames)")
+                    help="frames queued back to back on one stream even for shards (no overlap of consecutive frames)")
+    ap.add_argument("--two-streams", action="store_true",
+                    help="frames on two streams even for the whole frame (default only for shards of N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
@@ -355,9 +357,11 @@ def main():
     W, H = args.width, args.height
     cam = pt.make_camera(width=W, height=H, **cam_kw)
     r = pt.Renderer(scene, device=local)
-    # two framebuffers (and, for frames queued back to back, two streams): frame k's RCCL reduce runs
-    # while frame k+1 renders into the other one
-    overlap = not args.sync_frames and not args.one_stream
+    # two framebuffers (and, for a shard of N > 1, two streams): frame k's RCCL reduce runs while frame
+    # k+1 renders into the other one.  On two streams frame k+1's seeding pre-pass runs beside frame k's
+    # last waves (its integration kernel still follows frame k's finalisation): +1.3% on the 1/8 C3 shard,
+    # +-0 on the whole frame, -9% on C2's 10-ms frames (the cross-stream wait), so shards only by default
+    overlap = not args.sync_frames and not args.one_stream and (args.two_streams or shards > 1)
     fbs = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(2 if (distributed or overlap) else 1)]
 
     def render(buf, flags=0):

@@ -3290,6 +3290,11 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             b.seed_states = B.seed_states;
         }
         hipLaunchKernelGGL(init_pixel_states, dim3((b.npix + 255) / 256), dim3(256), 0, stream, b, B.pix_states);
+        // A render queued on another stream while one is in flight: its seeding pre-pass runs beside the
+        // earlier render's last waves (its own buffers), but the integration kernel waits until the earlier
+        // render is complete (finalisation included), so a persistent grid never takes the CU slots an
+        // earlier frame's finalisation needs (that one would otherwise wait out the whole next frame)
+        if (c->fl_n > 0) HIP_TRY(hipStreamWaitEvent(stream, c->fl[(c->fl_head + c->fl_n - 1) % pt_ctx::kFlights].ev1, 0));
         HIP_TRY(hipEventRecord(F.ek0, stream));
         kernel_events = true;
         units = b.nunits;
