@@ -39,8 +39,9 @@ out = {
 }
 if "GRBM_GUI_ACTIVE" in c:
     cyc = c["GRBM_GUI_ACTIVE"] / 8.0     # summed over the 8 XCDs
-    b = {"limiter": "dependent memory round trips per walk step and shading pass (DESIGN.md 6); "
-                    "VALU issue and TD busy near their nominal rates",
+    b = {"limiter": "a serial chain per walk step -- the node's memory round trip, then the dependent VALU that "
+                    "picks the next address -- and per shading pass (DESIGN.md 6); TD busy counts requests in "
+                    "flight, VALU issue is about half its wave64 rate",
          "cycles_per_launch": int(cyc)}
     if "SQ_INSTS_VALU" in c:
         # wave64 VALU instructions per SIMD-cycle; the nominal rate is 0.25 (4 cycles per wave64 op),
