@@ -1472,24 +1472,29 @@ __device__ __forceinline__ uint32_t take_unit(const Args& a, int lane, uint64_t 
 // keeps the path vertices; the connection weights are recomputed from them in the sample's last pass,
 // in the reference's order, with the visibility bits the shadow walks left (the weights' arithmetic
 // is identical both times, so the set of connections that trace cannot differ).
+// Cells are grouped by the pass that reads them, so that a pass touches few cells (a wave's access to
+// one word of a cell spans the same 1 KiB as the whole cell): every pass reads cell 0 only, the
+// sample's last pass cells 10-12.
 enum : int {
-    HW_N = 0, HW_STAGE, HW_FLAGS, HW_RNG_D,   // cell 0: sample, stage word, flags, XORWOW d
+    HW_N = 0, HW_SF, HW_RNG_D, HW_CU1,        // cell 0: sample, stage | flags << 16, XORWOW d, the pending
+                                              //         visibility ray's length
     HW_RNG_V0 = 4,                            // cell 1: v0..v3
-    HW_RNG_V4 = 8, HW_NEND, HW_CU1, HW_CU2,   // cell 2: v4, unit end, the cosine draws (CU1: the pending
-                                              //         visibility ray's length once T3 has begun)
+    HW_RNG_V4 = 8, HW_NEND, HW_DU1, HW_DU2,   // cell 2: v4, unit end, the cosine draws of T3
     HW_X0 = 12, HW_MAT0 = 15,                 // cell 3: light vertex x0 (offset along its normal), material
     HW_N0 = 16, HW_IP1 = 19,                  // cell 4: its normal, ip[1]
     HW_X1 = 20, HW_MAT1 = 23,                 // cell 5: light bounce hit x1, material
-    HW_N1 = 24, HW_IP2 = 27,                  // cell 6: its normal, ip[2]
+    HW_N1 = 24,                               // cell 6: its normal
     HW_X3 = 28, HW_MAT3 = 31,                 // cell 7: camera hit x3, material
-    HW_N3 = 32, HW_MAT2 = 35,                 // cell 8: its normal, material of x2
-    HW_X2 = 36, HW_G1 = 39,                   // cell 9: camera bounce hit x2, G of the light subpath edge x1-x0
+    HW_N3 = 32,                               // cell 8: its normal
+    HW_X2 = 36,                               // cell 9: camera bounce hit x2
     HW_GC = 40,                               // cell 10: G of the four connections (written with T3's end)
-    HW_M = 44, HW_G3 = 50,                    // cells 11, 12.lo: running mean m0..m2 (f64); 12.z: G of x3-x2
-    HW_PXY = 52, HW_Q, HW_MTRI, HW_MT,        // cell 13: pixel (x | y << 16), split slot, primary memo (tri, t)
-    HW_CD = 56,                               // cell 14: camera direction (pinhole: the unit's; lens: the sample's)
-    HW_CO = 60,                               // cell 15: camera origin of a lens sample
-    kHeadWords = 64
+    HW_FA = 44,                               // cell 11: G1, G3, ip[1], ip[2] (T3's end)
+    HW_FB = 48,                               // cell 12: the four materials (T3's end)
+    HW_M = 52,                                // cells 13, 14.lo: running mean m0..m2 (f64)
+    HW_PXY = 60, HW_Q, HW_MTRI, HW_MT,        // cell 15: pixel (x | y << 16), split slot, primary memo (tri, t)
+    HW_CD = 64,                               // cell 16: camera direction (pinhole: the unit's; lens: the sample's)
+    HW_CO = 68,                               // cell 17: camera origin of a lens sample
+    kHeadWords = 72
 };
 // stage word: bits 0-1 the pending trace, 2-3 the connection whose visibility ray it is (k = 2i + j-2),
 // 4-7 visibility bits, 8-11 the connections that need a ray
@@ -1596,7 +1601,6 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     // (the XORWOW words v0..v3 are read and written only where a sample starts -- the only place a
     // sample draws -- so they are not live across the pass: the shading code then fits 96 VGPRs)
     const uint4 k0 = R.ld4(HW_N);
-    const uint32_t k2z = R.ld(HW_CU1);
     if (state == ST_CHECK) {
         SEC(SEC_CHECK);
         const float4 C = a.acc_tris[htri].c;
@@ -1605,12 +1609,12 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
         state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
     }
     int n = (int)k0.x;
-    uint32_t stage = k0.y, fl = k0.z;
+    uint32_t stage = k0.y & 0xffffu, fl = k0.y >> 16;
     Rng rng;
-    rng.d = k0.w;
+    rng.d = k0.z;
     // (likewise v4, the unit end and the cosine draws: each read where it is used, written where it
     // changes; only cell 0 -- n, stage, flags, XORWOW d -- is live across the pass)
-    float cu1 = __uint_as_float(k2z);   // the pending visibility ray's length (its check below)
+    float cu1 = __uint_as_float(k0.w);   // the pending visibility ray's length (its check below)
     // (the staged light records and, behind them, each one's normal and material)
     const DLight* const llt = reinterpret_cast<const DLight*>(lprobe + 4 + kMaxProbeEmitters * 12);
     const float4* const lnm = reinterpret_cast<const float4*>(lprobe + 4 + kMaxProbeEmitters * 12 + kLdsLights * 12);
@@ -1699,7 +1703,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
         const float du1 = rng_uniform(rng);   // cosine_ray's draws for T3 (kernel.cu:307)
         const float du2 = rng_uniform(rng);
         R.st(HW_RNG_V4, rng.v4);
-        R.st2(HW_CU1, __float_as_uint(du1), __float_as_uint(du2));
+        R.st2(HW_DU1, __float_as_uint(du1), __float_as_uint(du2));
         R.st4(HW_RNG_V0, rng.v0, rng.v1, rng.v2, rng.v3);
         R.st4(HW_X0, __float_as_uint(ro.x), __float_as_uint(ro.y), __float_as_uint(ro.z), (uint32_t)m0);
         R.st4(HW_N0, __float_as_uint(n0.x), __float_as_uint(n0.y), __float_as_uint(n0.z), 0u);
@@ -1752,8 +1756,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     auto vis_stage = [&](uint32_t k, V3 xi, V3 xj) -> bool {
         float len;
         head_vis_ray(xi, xj, &ro, &rd, &len);
-        cu1 = len;   // (its walk may end in this pass: a root miss, no triangles)
-        R.st(HW_CU1, __float_as_uint(len));
+        cu1 = len;   // (stored with cell 0 at the pass's end; its walk may end in this pass: a root miss)
         stage = (stage & ~0xfu) | HS_SH | (k << 2);
         wave_count(lcnt + 1, lane);
         return begin_trace(head_vis_bound(len), head_vis_occluded(len));
@@ -1804,7 +1807,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 R.st4(HW_N3, __float_as_uint(n3.x), __float_as_uint(n3.y), __float_as_uint(n3.z), 0u);
                 // the camera bounce: cosine_ray (kernel.cu:78-99) with the draws taken at the start
                 SEC(SEC_COSINE);
-                const uint2 cc = R.ld2(HW_CU1);
+                const uint2 cc = R.ld2(HW_DU1);
                 const float du1 = __uint_as_float(cc.x), du2 = __uint_as_float(cc.y);
                 const float r = sqrtf(du1);
                 const float theta = (float)(2 * 3.14159 * (double)du2);
@@ -1839,11 +1842,10 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 const float ip[3] = {fresh(a.total_light_area), __uint_as_float(c4.w), (float)(3.14159 / (double)G)};
                 HeadGeo g;
                 head_geometry(x, nrm, g);
-                R.st4(HW_X2, __float_as_uint(x[2].x), __float_as_uint(x[2].y), __float_as_uint(x[2].z), __float_as_uint(g.G1));
+                R.st4(HW_X2, __float_as_uint(x[2].x), __float_as_uint(x[2].y), __float_as_uint(x[2].z), 0u);
                 R.st4(HW_GC, __float_as_uint(g.Gc[0]), __float_as_uint(g.Gc[1]), __float_as_uint(g.Gc[2]), __float_as_uint(g.Gc[3]));
-                R.st(HW_G3, __float_as_uint(g.G3));
-                R.st(HW_IP2, __float_as_uint(ip[2]));
-                R.st(HW_MAT2, (uint32_t)mat[2]);
+                R.st4(HW_FA, __float_as_uint(g.G1), __float_as_uint(g.G3), __float_as_uint(ip[1]), __float_as_uint(ip[2]));
+                R.st4(HW_FB, (uint32_t)mat[0], (uint32_t)mat[1], (uint32_t)mat[2], (uint32_t)mat[3]);
                 uint32_t need = 0;
                 acc = head_weights(a, mat, ip, g, 0u, &need);
                 if (need == 0u) {
@@ -1877,13 +1879,13 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 }
                 // the sample's last pass: the weights again, now with the visibility bits
                 HeadGeo g;
-                const uint4 gc = R.ld4(HW_GC);
+                const uint4 gc = R.ld4(HW_GC), fa = R.ld4(HW_FA), fb = R.ld4(HW_FB);
                 g.Gc[0] = __uint_as_float(gc.x); g.Gc[1] = __uint_as_float(gc.y); g.Gc[2] = __uint_as_float(gc.z);
                 g.Gc[3] = __uint_as_float(gc.w);
-                g.G1 = __uint_as_float(R.ld(HW_G1));
-                g.G3 = __uint_as_float(R.ld(HW_G3));
-                const int32_t mat[4] = {(int32_t)R.ld(HW_MAT0), (int32_t)R.ld(HW_MAT1), (int32_t)R.ld(HW_MAT2), (int32_t)R.ld(HW_MAT3)};
-                const float ip[3] = {fresh(a.total_light_area), __uint_as_float(R.ld(HW_IP1)), __uint_as_float(R.ld(HW_IP2))};
+                g.G1 = __uint_as_float(fa.x);
+                g.G3 = __uint_as_float(fa.y);
+                const int32_t mat[4] = {(int32_t)fb.x, (int32_t)fb.y, (int32_t)fb.z, (int32_t)fb.w};
+                const float ip[3] = {fresh(a.total_light_area), __uint_as_float(fa.z), __uint_as_float(fa.w)};
                 acc = head_weights(a, mat, ip, g, (stage >> 4) & 15u, nullptr);
                 sample_done = true;
             }
@@ -1987,7 +1989,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
         }
     }
     SEC(SEC_RECORD);
-    R.st4(HW_N, (uint32_t)n, stage, fl, rng.d);
+    R.st4(HW_N, (uint32_t)n, stage | (fl << 16), rng.d, __float_as_uint(cu1));
 }
 
 // The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
