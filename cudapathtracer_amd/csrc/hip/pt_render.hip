@@ -1880,6 +1880,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 // the sample's last pass: the weights again, now with the visibility bits
                 HeadGeo g;
                 const uint4 gc = R.ld4(HW_GC), fa = R.ld4(HW_FA), fb = R.ld4(HW_FB);
+
                 g.Gc[0] = __uint_as_float(gc.x); g.Gc[1] = __uint_as_float(gc.y); g.Gc[2] = __uint_as_float(gc.z);
                 g.Gc[3] = __uint_as_float(gc.w);
                 g.G1 = __uint_as_float(fa.x);
@@ -1894,9 +1895,12 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
             wave_count(lcnt + 2, lane);
             SEC(SEC_SAMPLE_END);
             const uint4 c13 = R.ld4(HW_PXY);
+            // the next sample's XORWOW words and the unit end, fetched with the sample's end
+            const uint4 r1 = R.ld4(HW_RNG_V0), r2 = R.ld4(HW_RNG_V4);
             const uint32_t px = c13.x & 0xffffu, py = c13.x >> 16;
             if (!(fl & CF_SPLIT)) {
-                const uint4 m01 = R.ld4(HW_M), m2 = R.ld4(HW_M + 4);
+                const uint4 m01 = R.ld4(HW_M);
+                const uint2 m2 = R.ld2(HW_M + 4);
                 const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;
                 const double x0 = dbl(m01.x, m01.y) * fn1, x1 = dbl(m01.z, m01.w) * fn1, x2 = dbl(m2.x, m2.y) * fn1;
                 double m0, mm1, mm2;
@@ -1926,13 +1930,14 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 Lb[0] = acc.r;
                 Lb[1] = acc.g;
                 Lb[2] = acc.b;
-                if ((uint32_t)n >= R.ld(HW_NEND)) {
+                if ((uint32_t)n >= r2.y) {
                     state = ST_IDLE;
                     break;
                 }
             }
             ++n;
-            again = start_sample(px, py, false);
+            rng.v0 = r1.x; rng.v1 = r1.y; rng.v2 = r1.z; rng.v3 = r1.w; rng.v4 = r2.x;
+            again = start_sample(px, py, true);
             break;
         }
       }
