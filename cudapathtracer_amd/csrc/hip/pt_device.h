@@ -958,7 +958,20 @@ struct NoSetup {
 #pragma clang diagnostic ignored "-Wsometimes-uninitialized"   // (a lane's triangle words, read only if it has a leaf)
 // kAnyHit: the walk ends at the first hit with t <= w.occ (integrator 1's visibility rays: any such hit
 // decides "occluded"; the winner check still runs on it).
-template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false>
+#ifdef PT_WIDE8
+constexpr bool kWide8 = true;
+#else
+constexpr bool kWide8 = false;
+#endif
+// kUniform (integrator 0's walks, the batched traces): every lane issues the triangle's loads and then the
+// node's, as buffer loads -- a lane without a triangle (or node) at an out-of-range offset, which reads
+// nothing and returns zeros -- so no exec-masked branch hides how many loads follow the triangle's: the
+// test waits for the triangle alone (vmcnt(7)) and runs under the node's round trip instead of after it
+// (the compiler had to wait for everything at the join behind the masked node loads).  The node is then
+// always read from memory, not from the LDS top (the top's hot lines hit L2): C3 +1.5% (5630 -> 5713,
+// same box, alternated, profiles/r03_uni).  Integrator 1 (kAnyHit) keeps the LDS top: bound by bytes, it
+// lost 2.7% this way.
+template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit && !kWide8>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
@@ -973,7 +986,17 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
     // other lanes' A, B, e2z are never read (pin_use below only orders the loads before the node's).
     float4 A, B;
     float e2z;
-    if (leaf) {
+    // (buffers of 2 GiB - 256 B: pt_create keeps the arrays far below; offset 2^31 is out of range)
+    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<DTri*>(tris), 0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<DNodeW*>(nodes), 0, 0x7fffff00, 0x00020000);
+    if constexpr (kUniform) {
+        const uint32_t tb = leaf ? __umul24(leaf4_slot(w), (uint32_t)sizeof(DTri)) : 0x80000000u;
+        const f4v a4 = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(trs, tb, 0, 0));
+        const f4v b4 = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(trs, tb + 16u, 0, 0));
+        A = make_float4(a4.x, a4.y, a4.z, a4.w);
+        B = make_float4(b4.x, b4.y, b4.z, b4.w);
+        e2z = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(trs, tb + 32u, 0, 0));
+    } else if (leaf) {
         const uint32_t tb = __umul24(leaf4_slot(w), (uint32_t)sizeof(DTri));
         A = glb_f4(tris, tb);
         B = glb_f4(reinterpret_cast<const char*>(tris) + 16, tb);
@@ -997,6 +1020,17 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
 #else
     float4 NX, FX, NY, FY, NZ, FZ;
     uint4 ch;
+    if constexpr (kUniform) {
+        const uint32_t nb = visit ? nidx * 128u : 0x80000000u;
+        auto bl = [&](uint32_t off) {
+            const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(nrs, off, 0, 0));
+            return make_float4(v.x, v.y, v.z, v.w);
+        };
+        const uint32_t ox = nb | w.nx, oy = nb | w.ny, oz = nb | w.nz;
+        NX = bl(ox); FX = bl(ox ^ 48u); NY = bl(oy); FY = bl(oy ^ 80u); NZ = bl(oz); FZ = bl(oz ^ 112u);
+        const float4 c4 = bl(nb + 96u);
+        ch = make_uint4(__float_as_uint(c4.x), __float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w));
+    } else {
     // Every lane reads the LDS copy first (a deep node's lane reads node 0: a broadcast), then the
     // deep nodes' lanes overwrite it with their global loads -- in this order, because the loads
     // write the same registers and an LDS read issued behind outstanding global loads to them
@@ -1019,10 +1053,11 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
         NZ = glb_f4(nodes, oz); FZ = glb_f4(nodes, oz ^ 112u);
         ch = glb_u4(nodes, nb + 96u);
     }
+    }
 #endif
     setup(w);
     pin_use(A); pin_use(B); pin_use1(e2z);   // (the node's fields feed unconditional tests: no pin needed)
-    if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
+    if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop && !kUniform) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
         const float t = tri_hit_pk(f2{o.x, o.y}, o.z, f2{d.x, d.y}, d.z, A, B, e2z);
         const uint32_t lslot = leaf4_slot(w);   // (recomputed here: one register less across the loads)
