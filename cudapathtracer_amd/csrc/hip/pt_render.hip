@@ -27,6 +27,8 @@ namespace {
 
 constexpr uint32_t kTile = 8;   // 8x8 = 64 pixels = one wave
 
+// A box is skipped when its entry lies beyond best_t * kCullRel (DESIGN.md "Traversal" 4)
+constexpr float kCullRel = 1.0f + 1.0f / 1024.0f;
 struct Args {
     const DNode* nodes;
     const RNode* rnodes;
@@ -1399,10 +1401,10 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
     // fresh walk is the only one at node 0.)  Nothing entered: the walk is over without a candidate,
     // as a finished walk would be; the lane shades in the next pass.
     if (a.root_first && state == ST_TRACE && w.node == 0u) {
-        bool more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        bool more = walk4_root<kCount>(w, S, kCullRel, a.node_mask, cnt);
         // (up to root_first visits: the next node too while it is staged in LDS and no leaf is queued)
         for (uint32_t k = 1; more && k < a.root_first && w.node < S.ntop && !leaf4_pending(w); ++k)
-            more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+            more = walk4_root<kCount>(w, S, kCullRel, a.node_mask, cnt);
         if (!more) state = (w.best_t == kMaxFloat) ? ST_SHADE : ST_SLOW;
     }
     SEC(SEC_RECORD);
@@ -1985,9 +1987,9 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
       if (__ballot(again) == 0ull) break;
     }
     if (a.root_first && state == ST_TRACE && w.node == 0u) {
-        bool more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+        bool more = walk4_root<kCount>(w, S, kCullRel, a.node_mask, cnt);
         for (uint32_t k = 1; more && k < a.root_first && w.node < S.ntop && !leaf4_pending(w); ++k)
-            more = walk4_root<kCount>(w, S, a.cull_rel, a.node_mask, cnt);
+            more = walk4_root<kCount>(w, S, kCullRel, a.node_mask, cnt);
         if (!more) {   // nothing below the bound: a miss
             w.best_t = kMaxFloat;
             state = ST_SHADE;
@@ -2081,10 +2083,14 @@ __device__ __forceinline__ void wf_main(const Args& a)
         if (kCount) clk0 = clock64();
         const uint64_t live = __ballot(state != ST_DONE);   // (no lane becomes DONE while walking)
         if (kCount) start_wait += (uint32_t)__popcll(live & ~__ballot(state == ST_TRACE));
+        // (the threshold as an opaque scalar: left a kernel argument, it was reloaded and waited for at
+        // the head of every step)
+        uint32_t thr;
+        asm volatile("s_mov_b32 %0, %1" : "=s"(thr) : "s"(a.wf_threshold));
         for (;;) {
             const uint64_t tracing = __ballot(state == ST_TRACE);
             if (tracing == 0ull) break;
-            if ((uint32_t)__popcll(live & ~tracing) >= a.wf_threshold) break;   // lanes waiting to shade
+            if ((uint32_t)__popcll(live & ~tracing) >= thr) break;   // lanes waiting to shade
             if (kCount) {
                 ++walk_slots;
                 if (state == ST_TRACE) ++trace_slots;
@@ -2098,7 +2104,9 @@ __device__ __forceinline__ void wf_main(const Args& a)
                 if (noleaf && deep == 0u) ++itc[5];
             }
             if (state == ST_TRACE) {
-                const bool more = walk4_step<kCount, true, NoSetup, kHead>(w, ro, rd, a.nodes4, a.acc_tris, S, a.cull_rel,
+                // (the culling factor as the literal it always is: a kernel argument here was a scalar
+                // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
+                const bool more = walk4_step<kCount, true, NoSetup, kHead>(w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel,
                                                                            a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
@@ -3067,7 +3075,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     a.tile_bx = tw / kTile; a.tile_blocks = (tw / kTile) * (th / kTile);
     a.morton_out = (p->pixel_order == PT_ORDER_MORTON) ? 1u : 0u;
     a.ntiles_shard = (ntiles > (uint32_t)p->shard_index) ? (ntiles - (uint32_t)p->shard_index + (uint32_t)p->shard_count - 1) / (uint32_t)p->shard_count : 0;
-    a.cull_rel = 1.0f + 1.0f / 1024.0f;
+    a.cull_rel = kCullRel;
     a.cull_abs = c->scene_extent * 1e-4f;
     const bool refwalk = (p->flags & PT_FLAG_REFERENCE_TRAVERSAL) != 0;
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
@@ -3555,7 +3563,7 @@ extern "C" int pt_trace_counts(pt_ctx* c, uint32_t n, const float* rays, int32_t
     a.sphere_mat_base = c->sphere_mat_base;
     memcpy(a.root, c->root, sizeof(a.root));
     memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
-    a.cull_rel = 1.0f + 1.0f / 1024.0f;
+    a.cull_rel = kCullRel;
     a.cull_abs = c->scene_extent * 1e-4f;
     a.scene_fast = c->scene_fast ? 1u : 0u;
     a.node_mask = c->node4_mask;
