@@ -3523,10 +3523,19 @@ static int ensure_spill(pt_ctx::Bufs& B, size_t words)
 
 static bool alloc_bufs(pt_ctx::Bufs& B)
 {
-    if (B.counters) return true;
-    return hipMalloc(reinterpret_cast<void**>(&B.counters), kCounterWords * sizeof(unsigned long long)) == hipSuccess &&
-           hipMalloc(reinterpret_cast<void**>(&B.tile_counter), 16) == hipSuccess &&
-           hipMalloc(reinterpret_cast<void**>(&B.pixel_counter), kQueueStride * (kQueues + 1) * 4) == hipSuccess;
+    if (B.counters && B.tile_counter && B.pixel_counter) return true;
+    // (all three or none: a partial failure is released, so the next call allocates again)
+    for (void** q : {reinterpret_cast<void**>(&B.counters), reinterpret_cast<void**>(&B.tile_counter),
+                     reinterpret_cast<void**>(&B.pixel_counter)})
+        if (*q) { (void)hipFree(*q); *q = nullptr; }
+    if (hipMalloc(reinterpret_cast<void**>(&B.counters), kCounterWords * sizeof(unsigned long long)) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&B.tile_counter), 16) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&B.pixel_counter), kQueueStride * (kQueues + 1) * 4) == hipSuccess)
+        return true;
+    for (void** q : {reinterpret_cast<void**>(&B.counters), reinterpret_cast<void**>(&B.tile_counter),
+                     reinterpret_cast<void**>(&B.pixel_counter)})
+        if (*q) { (void)hipFree(*q); *q = nullptr; }
+    return false;
 }
 
 extern "C" int pt_trace(pt_ctx* c, uint32_t n, const float* rays, int32_t* tri_out, float* t_out, uint32_t flags)
