@@ -2734,6 +2734,14 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                 if (new_of[o] == ~0u) { new_of[o] = (uint32_t)old_of.size(); old_of.push_back(o); }
         }
         c->top_nodes = std::min(std::max(c->wf_top, 1u), n4);   // (>= 1: the wavefront walk reads the LDS top unconditionally)
+        // A tree the LDS top holds whole (small scenes: C2's Cornell box) is walked with no node fetch
+        // from memory, so a walk step is cheap: waves stay in the walk phase until 62 lanes wait to
+        // shade, and a new ray's first two visits (not four) run in the shading pass (C2: 6879 -> 7081
+        // Msamples/s, same box, profiles/r03_c2_knobs; the stand-in's defaults are unchanged).
+        if (n4 <= c->top_nodes) {
+            if (!getenv("PT_WF_THRESHOLD")) c->wf_threshold = 62;
+            if (!getenv("PT_WF_ROOT_FIRST")) c->wf_root_first = 2;
+        }
         an.resize(n4);
         // Triangle slots: the triangles of each node's leaf children (in node order) get consecutive
         // slots, and each node lists its leaf children first -- the walk queues a node's entered
