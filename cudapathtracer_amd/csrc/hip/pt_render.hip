@@ -2000,7 +2000,9 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
 }
 
 // The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
-template <bool kCount, bool kHead>
+// kLdsWalk: walk steps read the staged top from LDS (integrator 1 always; integrator 0 when the LDS
+// top holds the whole tree) instead of issuing every node's loads to memory.
+template <bool kCount, bool kHead, bool kLdsWalk = kHead>
 __device__ __forceinline__ void wf_main(const Args& a)
 {
     extern __shared__ uint32_t lds_wf[];
@@ -2106,8 +2108,8 @@ __device__ __forceinline__ void wf_main(const Args& a)
             if (state == ST_TRACE) {
                 // (the culling factor as the literal it always is: a kernel argument here was a scalar
                 // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
-                const bool more = walk4_step<kCount, true, NoSetup, kHead>(w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel,
-                                                                           a.cull_abs, a.node_mask, cnt);
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk && !kWide8>(
+                    w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
                     atomicAdd(lhist + min(31 - __clz((int)steps), kHist - 1), 1u);
@@ -2193,10 +2195,10 @@ __device__ __forceinline__ void wf_main(const Args& a)
     }
 }
 
-template <bool kCount, int kMinWaves>
+template <bool kCount, int kMinWaves, bool kLdsWalk = false>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
-    wf_main<kCount, false>(a);
+    wf_main<kCount, false, kLdsWalk>(a);
 }
 
 // integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the wavefront state machine
@@ -2453,6 +2455,8 @@ struct pt_ctx {
     bool head_wf = true;            // integrator 1 on the wavefront kernel (PT_HEAD_WF=0: the tile kernel)
     int head_min_waves = 5;         // its register budget (PT_HEAD_MIN_WAVES: 4 = 128 VGPRs, 5 = 96)
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
+    uint32_t n4 = 0;                // nodes of this scene's BVH4
+    bool wf_lds_tree = true;        // (PT_WF_LDS_TREE)
     DNodeW* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
@@ -2734,6 +2738,8 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                 if (new_of[o] == ~0u) { new_of[o] = (uint32_t)old_of.size(); old_of.push_back(o); }
         }
         c->top_nodes = std::min(std::max(c->wf_top, 1u), n4);   // (>= 1: the wavefront walk reads the LDS top unconditionally)
+        c->n4 = n4;
+        if (const char* e = getenv("PT_WF_LDS_TREE")) c->wf_lds_tree = atoi(e) != 0;
         // A tree the LDS top holds whole (small scenes: C2's Cornell box) is walked with no node fetch
         // from memory, so a walk step is cheap: waves stay in the walk phase until 62 lanes wait to
         // shade, and a new ray's first two visits (not four) run in the shading pass (C2: 6879 -> 7081
@@ -3153,6 +3159,9 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             if (b.top_nodes > 0) b.top_nodes = std::max(1u, std::min(b.top_nodes, cap));   // (0: no triangles, no BVH4)
         }
         const size_t lds_wf = lds_fixed + (size_t)b.top_nodes * kTopNodeBytes;
+        // the whole tree staged in LDS (small scenes: C2): integrator 0's walk steps read it there too
+        // (PT_WF_LDS_TREE=0: memory loads, as for a tree larger than the top)
+        const bool lds_tree = c->wf_lds_tree && c->n4 > 0 && b.top_nodes >= c->n4;
         uint32_t blocks = (uint32_t)c->num_cus * (wpc / 4 ? wpc / 4 : 1);
         // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
         // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`
@@ -3330,6 +3339,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         else if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (c->wf_min_waves == 5 && lds_tree) hipLaunchKernelGGL((render_unidir_wf<false, 5, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());
