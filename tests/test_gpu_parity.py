@@ -97,6 +97,22 @@ def test_ragged_images_and_depths(oracle_mod, w, h, spp, bounces):
     assert st["rays_reference"] == cnt["traces"]
 
 
+@pytest.mark.parametrize("lds_tree", ["1", "0"])
+def test_tree_held_whole_in_lds(oracle_mod, monkeypatch, lds_tree):
+    """A tree the LDS top holds whole (the Cornell box, C2's scene): integrator 0's walk steps read
+    it from LDS (render_unidir_wf<false, 5, true>, with walk threshold 62 and two root-first visits)
+    or, with PT_WF_LDS_TREE=0, from memory like a large tree's -- both bit-exact, both integrators."""
+    monkeypatch.setenv("PT_WF_LDS_TREE", lds_tree)
+    s = load_scene("cornell")
+    w, h, spp = 24, 24, 4
+    with pt.Renderer(s, 0) as r:
+        for integ in (0, 1):
+            img, st = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=8, integrator=integ)
+            ref, cnt = _oracle(oracle_mod, s, w, h, spp, 8, integ)
+            assert _bits_equal(img, ref) == 0, integ
+            assert st["rays_reference"] == cnt["traces"]
+
+
 def test_lens_radius_and_seed(oracle_mod, cb):
     """radius > 0 consumes the two lens draws per sample from the pixel's stream (decision d1)."""
     s, r = cb
