@@ -3337,6 +3337,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             else hipLaunchKernelGGL((render_head_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         }
         else if (count && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<true, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (count && lds_tree) hipLaunchKernelGGL((render_unidir_wf<true, 5, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5 && lds_tree) hipLaunchKernelGGL((render_unidir_wf<false, 5, true>), dim3(blocks), dim3(256), lds_wf, stream, b);

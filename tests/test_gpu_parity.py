@@ -111,6 +111,13 @@ def test_tree_held_whole_in_lds(oracle_mod, monkeypatch, lds_tree):
             ref, cnt = _oracle(oracle_mod, s, w, h, spp, 8, integ)
             assert _bits_equal(img, ref) == 0, integ
             assert st["rays_reference"] == cnt["traces"]
+            # the counting variant walks the same way: the same image, and (LDS walk) every node visit an LDS read
+            img2, st2 = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=8, integrator=integ,
+                                 flags=pt.PT_FLAG_COUNT)
+            assert _bits_equal(img2, ref) == 0, integ
+            assert st2["node_tests"] > 0
+            if integ == 0 and lds_tree == "1":
+                assert st2["lds_node_tests"] == st2["node_tests"]
 
 
 def test_lens_radius_and_seed(oracle_mod, cb):
