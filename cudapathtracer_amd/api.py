@@ -148,9 +148,17 @@ def write_ppm(path, img, pixel_order=0, width=None, height=None):
     (W*H, 3) float32 buffer (pixel_order=PT_ORDER_MORTON, width/height given)."""
     img = np.ascontiguousarray(img)
     if pixel_order == L.PT_ORDER_MORTON:
+        if width is None or height is None:
+            raise ValueError("write_ppm: a Morton-ordered buffer needs width and height")
+        width, height = int(width), int(height)
+        if width <= 0 or height <= 0 or img.size != width * height * 3:
+            raise ValueError("write_ppm: Morton buffer holds %d values, width*height*3 = %d"
+                             % (img.size, max(width, 0) * max(height, 0) * 3))
         img = np.ascontiguousarray(img, dtype=np.float32)
-        L.check(L.lib().pt_write_ppm_order(str(path).encode(), img.ctypes.data, int(width), int(height), 1))
+        L.check(L.lib().pt_write_ppm_order(str(path).encode(), img.ctypes.data, width, height, 1))
         return
+    if pixel_order != L.PT_ORDER_SCANLINE:
+        raise ValueError("write_ppm: unknown pixel_order %r" % (pixel_order,))
     h, w = img.shape[:2]
     if img.dtype == np.float64:
         L.check(L.lib().pt_write_ppm_f64(str(path).encode(), img.ctypes.data, w, h))

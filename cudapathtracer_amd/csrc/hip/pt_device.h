@@ -502,25 +502,6 @@ struct alignas(16) DNode4 {
     uint4 pad;
 };
 static_assert(sizeof(DNode4) == 128, "BVH4 node is 128 B");
-#ifdef PT_WIDE8
-// Experiment (PT_WIDE8 builds, tools/build_variants.sh): the render path's tree collapsed 8 wide, each
-// node one 128-B line with its child boxes quantized -- per axis an origin and a power-of-two step,
-// each child plane one byte on that grid rounded outward, so the decoded box contains the inflated box
-// (the same exactness argument as the float boxes: DESIGN.md "Traversal").  A plane's distance is
-// fma(q, 2^e * inv, fma(origin, inv, -o * inv)): 2^e * inv is exact, the two roundings are far below
-// the margin.  An empty slot is an inverted box (lo byte 255, hi byte 0) with a leaf word of empty mask,
-// which adds nothing should rounding ever let a ray "enter" it.
-struct alignas(16) DNode8 {
-    float4 hdr;        // origin x, y, z; w: the step exponents as bytes (e + 128), x | y << 8 | z << 16
-    uint4 qx, qy, qz;  // per axis: lo bytes of children 0-3, of 4-7, hi bytes of 0-3, of 4-7
-    uint4 c0, c1;      // child words 0-3, 4-7 (as DNode4::child)
-    uint4 pad[2];
-};
-static_assert(sizeof(DNode8) == 128, "8-wide node is one 128-B line");
-using DNodeW = DNode8;
-#else
-using DNodeW = DNode4;
-#endif
 constexpr uint32_t kEmpty = 0xffffffffu;
 constexpr uint32_t kNone = 0xffffffffu;    // no node / no leaf pending
 constexpr int kLeafRing = 4;               // LDS leaf-queue entries per lane (one per node with entered leaves)
@@ -605,15 +586,9 @@ __device__ __forceinline__ void walk4_setup(W4& w, V3 o, V3 d)
     if (d.y == 0.0f) w.inv.y = __builtin_copysignf(0x1p100f, d.y);
     if (d.z == 0.0f) w.inv.z = __builtin_copysignf(0x1p100f, d.z);
     w.oi = v3(o.x * w.inv.x, o.y * w.inv.y, o.z * w.inv.z);
-#ifdef PT_WIDE8
-    w.nx = (w.inv.x < 0.0f) ? 1u : 0u;     // the near plane per axis is the hi byte
-    w.ny = (w.inv.y < 0.0f) ? 1u : 0u;
-    w.nz = (w.inv.z < 0.0f) ? 1u : 0u;
-#else
     w.nx = (w.inv.x < 0.0f) ? 48u : 0u;    // hix : lox  (the far plane is at nx ^ 48)
     w.ny = (w.inv.y < 0.0f) ? 64u : 16u;   // hiy : loy  (ny ^ 80)
     w.nz = (w.inv.z < 0.0f) ? 80u : 32u;   // hiz : loz  (nz ^ 112)
-#endif
 }
 // Only rays satisfying ray_fast() walk the BVH4 (all exact tests use Markstein quotients);
 // the others take trace_slow() below.  Returns the conservative root test.
@@ -756,11 +731,7 @@ constexpr int kWaveLdsWords = (kRing + kLeafRing) * 64;
 // by the wavefront kernel, 112 B each (the node without its pad; stride 28 dwords, so 16
 // consecutive nodes occupy disjoint banks): lanes visiting them read LDS instead of issuing
 // vector-memory loads -- the kernel's limiting pipe (TA/TD, DESIGN.md "Measurement").
-#ifdef PT_WIDE8
-constexpr uint32_t kTopNodeBytes = 96;    // (the 8-wide node without its pad)
-#else
 constexpr uint32_t kTopNodeBytes = 112;
-#endif
 // what fits next to the rings with 5 blocks of 256 threads per CU: LDS is granted in 1280-B granules,
 // 32000 B per block = 4 x 5120 B of rings + 160 B of counters + 208 B of light-probe emitters
 // (pt_render.hip) + 240 B of NEE light records + 97 x 112 B
@@ -844,86 +815,6 @@ __device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX
     }
     w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
 }
-#ifdef PT_WIDE8
-// One 8-wide node visit (the quantized node's fields): the eight box tests, the entered leaves queued as
-// one entry, the entered inner children pushed far-to-near, the nearest one next.
-__device__ __forceinline__ float ubyte_f(uint32_t x, int b)   // v_cvt_f32_ubyte{b}
-{
-    return (float)((x >> (8 * b)) & 255u);
-}
-template <bool kCount>
-__device__ __forceinline__ void visit8(W4& w, const float4& H, const uint4& QX, const uint4& QY, const uint4& QZ,
-                                       const uint4& C0, const uint4& C1, const Stack4& S, float cull_rel,
-                                       uint32_t node_mask, Counters& cnt)
-{
-    const float lim = w.best_t * cull_rel;
-    const uint32_t eb = __float_as_uint(H.w);
-    const float sx = __builtin_ldexpf(w.inv.x, (int)(eb & 255u) - 128);
-    const float sy = __builtin_ldexpf(w.inv.y, (int)((eb >> 8) & 255u) - 128);
-    const float sz = __builtin_ldexpf(w.inv.z, (int)((eb >> 16) & 255u) - 128);
-    const float bx = __builtin_fmaf(H.x, w.inv.x, -w.oi.x), by = __builtin_fmaf(H.y, w.inv.y, -w.oi.y),
-                bz = __builtin_fmaf(H.z, w.inv.z, -w.oi.z);
-    // near / far byte words per axis (the hi bytes are the near planes where inv < 0)
-    const bool fx = w.nx != 0u, fy = w.ny != 0u, fz = w.nz != 0u;
-    const uint32_t nx0 = fx ? QX.z : QX.x, nx1 = fx ? QX.w : QX.y, gx0 = fx ? QX.x : QX.z, gx1 = fx ? QX.y : QX.w;
-    const uint32_t ny0 = fy ? QY.z : QY.x, ny1 = fy ? QY.w : QY.y, gy0 = fy ? QY.x : QY.z, gy1 = fy ? QY.y : QY.w;
-    const uint32_t nz0 = fz ? QZ.z : QZ.x, nz1 = fz ? QZ.w : QZ.y, gz0 = fz ? QZ.x : QZ.z, gz1 = fz ? QZ.y : QZ.w;
-    const uint32_t r[8] = {C0.x, C0.y, C0.z, C0.w, C1.x, C1.y, C1.z, C1.w};
-    uint32_t key[8];
-    uint32_t lw = 0u;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {   // children 2p, 2p + 1 (one packed FMA per plane pair)
-        const uint32_t NXw = p < 2 ? nx0 : nx1, NYw = p < 2 ? ny0 : ny1, NZw = p < 2 ? nz0 : nz1;
-        const uint32_t FXw = p < 2 ? gx0 : gx1, FYw = p < 2 ? gy0 : gy1, FZw = p < 2 ? gz0 : gz1;
-        const int b0 = (2 * p) & 3, b1 = b0 + 1;
-        const f2 ax = pk_fma(f2{ubyte_f(NXw, b0), ubyte_f(NXw, b1)}, sx, bx);
-        const f2 ay = pk_fma(f2{ubyte_f(NYw, b0), ubyte_f(NYw, b1)}, sy, by);
-        const f2 az = pk_fma(f2{ubyte_f(NZw, b0), ubyte_f(NZw, b1)}, sz, bz);
-        const f2 gx = pk_fma(f2{ubyte_f(FXw, b0), ubyte_f(FXw, b1)}, sx, bx);
-        const f2 gy = pk_fma(f2{ubyte_f(FYw, b0), ubyte_f(FYw, b1)}, sy, by);
-        const f2 gz = pk_fma(f2{ubyte_f(FZw, b0), ubyte_f(FZw, b1)}, sz, bz);
-        const float t0 = entry4(ax.x, ay.x, az.x), t1 = entry4(ax.y, ay.y, az.y);
-        const bool e0 = t0 <= exit4(gx.x, gy.x, gz.x, lim), e1 = t1 <= exit4(gx.y, gy.y, gz.y, lim);
-        const uint32_t r0 = r[2 * p], r1 = r[2 * p + 1];
-        const bool l0 = (int32_t)r0 < 0, l1 = (int32_t)r1 < 0;
-        lw |= (e0 && l0 ? r0 : 0u) | (e1 && l1 ? r1 : 0u);
-        key[2 * p] = (e0 && !l0) ? ((__float_as_uint(t0) & ~node_mask) | r0) : kNone;
-        key[2 * p + 1] = (e1 && !l1) ? ((__float_as_uint(t1) & ~node_mask) | r1) : kNone;
-    }
-    if ((lw & ((1u << kLeafBits) - 1u)) != 0u) {
-        const uint32_t e = lw & ~kLeaf;
-        if (!leaf4_pending(w)) w.leaf = e;
-        else { S.ring[(kRing + w.lsp) * 64] = e; ++w.lsp; }
-    }
-    // Batcher's odd-even merge sort of the eight keys (19 compare-exchanges)
-    auto cx = [&](int i, int j) { const uint32_t lo = min(key[i], key[j]); key[j] = max(key[i], key[j]); key[i] = lo; };
-    cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
-    cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
-    cx(1, 2); cx(5, 6);
-    cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
-    cx(2, 4); cx(3, 5);
-    cx(1, 2); cx(3, 4); cx(5, 6);
-    // keys 1..V-1 (V valid, a sorted prefix) pushed far-to-near: key i to slot sp + V - 1 - i; an
-    // invalid key i >= V to the free slot sp + i - 1 (above the new top) -- no wrap possible while
-    // sp <= kRing - 7 in every lane
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 1; i < 8; ++i) v += (key[i] != kNone) ? 1u : 0u;   // valid keys beyond the first
-    if (__ballot(w.sp > kRing - 7) == 0ull) {
-#pragma unroll
-        for (int i = 1; i < 8; ++i) {
-            const int slot = ((uint32_t)i <= v) ? w.sp + (int)v - i : w.sp + i - 1;
-            S.ring[slot * 64] = key[i];
-        }
-        w.sp += (int)v;
-    } else {
-#pragma unroll
-        for (int i = 7; i >= 1; --i)
-            if (key[i] != kNone) push4<kCount>(w, S, key[i], cnt);
-    }
-    w.node = (key[0] != kNone) ? (key[0] & node_mask) : kNone;
-}
-#endif
 // After a step: take the next queued leaf entry when the pending one is done, and pop the next stack
 // entry not culled by the best hit when there is no node to visit.
 __device__ __forceinline__ void advance4(W4& w, const Stack4& S, float cull_rel, uint32_t node_mask)
@@ -958,11 +849,6 @@ struct NoSetup {
 #pragma clang diagnostic ignored "-Wsometimes-uninitialized"   // (a lane's triangle words, read only if it has a leaf)
 // kAnyHit: the walk ends at the first hit with t <= w.occ (integrator 1's visibility rays: any such hit
 // decides "occluded"; the winner check still runs on it).
-#ifdef PT_WIDE8
-constexpr bool kWide8 = true;
-#else
-constexpr bool kWide8 = false;
-#endif
 // kUniform (integrator 0's walks, the batched traces): every lane issues the triangle's loads and then the
 // node's, as buffer loads -- a lane without a triangle (or node) at an out-of-range offset, which reads
 // nothing and returns zeros -- so no exec-masked branch hides how many loads follow the triangle's: the
@@ -971,8 +857,8 @@ constexpr bool kWide8 = false;
 // always read from memory, not from the LDS top (the top's hot lines hit L2): C3 +1.5% (5630 -> 5713,
 // same box, alternated, profiles/r03_uni).  Integrator 1 (kAnyHit) keeps the LDS top: bound by bytes, it
 // lost 2.7% this way.
-template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit && !kWide8>
-__device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __restrict__ nodes,
+template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit>
+__device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
                                            const Setup& setup = Setup())
@@ -988,7 +874,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
     float e2z;
     // (buffers of 2 GiB - 256 B: pt_create keeps the arrays far below; offset 2^31 is out of range)
     const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<DTri*>(tris), 0, 0x7fffff00, 0x00020000);
-    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<DNodeW*>(nodes), 0, 0x7fffff00, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<DNode4*>(nodes), 0, 0x7fffff00, 0x00020000);
     if constexpr (kUniform) {
         const uint32_t tb = leaf ? __umul24(leaf4_slot(w), (uint32_t)sizeof(DTri)) : 0x80000000u;
         const f4v a4 = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(trs, tb, 0, 0));
@@ -1004,20 +890,6 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
     }
     // a lane with no node to visit reads node 0 (the LDS copy when there is one)
     const uint32_t nidx = visit ? w.node : 0u;
-#ifdef PT_WIDE8
-    float4 H;
-    uint4 QX, QY, QZ, C0, C1;
-    if (kTop || S.ntop != 0u) {
-        const uint32_t mb = lds_addr(S.top) + __umul24(nidx < S.ntop ? nidx : 0u, kTopNodeBytes);
-        H = lds_f4a(mb); QX = lds_u4a(mb + 16u); QY = lds_u4a(mb + 32u); QZ = lds_u4a(mb + 48u);
-        C0 = lds_u4a(mb + 64u); C1 = lds_u4a(mb + 80u);
-    }
-    if (nidx >= S.ntop) {
-        const uint32_t nb = nidx * 128u;
-        H = glb_f4(nodes, nb); QX = glb_u4(nodes, nb + 16u); QY = glb_u4(nodes, nb + 32u); QZ = glb_u4(nodes, nb + 48u);
-        C0 = glb_u4(nodes, nb + 64u); C1 = glb_u4(nodes, nb + 80u);
-    }
-#else
     float4 NX, FX, NY, FY, NZ, FZ;
     uint4 ch;
     if constexpr (kUniform) {
@@ -1054,7 +926,6 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
         ch = glb_u4(nodes, nb + 96u);
     }
     }
-#endif
     setup(w);
     pin_use(A); pin_use(B); pin_use1(e2z);   // (the node's fields feed unconditional tests: no pin needed)
     if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop && !kUniform) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
@@ -1071,11 +942,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNodeW* __re
         }
         w.leaf &= w.leaf - 1u;   // that leaf is done
     }
-#ifdef PT_WIDE8
-    if (visit) visit8<kCount>(w, H, QX, QY, QZ, C0, C1, S, cull_rel, node_mask, cnt);
-#else
     if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
-#endif
     advance4(w, S, cull_rel, node_mask);
     if (kAnyHit && w.best_t <= w.occ) return false;
     return w.node != kNone || leaf4_pending(w);
@@ -1090,13 +957,6 @@ template <bool kCount>
 __device__ __forceinline__ bool walk4_root(W4& w, const Stack4& S, float cull_rel, uint32_t node_mask, Counters& cnt)
 {
     const uint32_t mb = lds_addr(S.top) + __umul24(w.node, kTopNodeBytes);   // node 0 (or a staged node: walk4_top)
-#ifdef PT_WIDE8
-    if (kCount) { ++cnt.nodes; ++cnt.top; }
-    visit8<kCount>(w, lds_f4a(mb), lds_u4a(mb + 16u), lds_u4a(mb + 32u), lds_u4a(mb + 48u), lds_u4a(mb + 64u),
-                   lds_u4a(mb + 80u), S, cull_rel, node_mask, cnt);
-    advance4(w, S, cull_rel, node_mask);
-    return w.node != kNone || leaf4_pending(w);
-#else
     const float4 NX = lds_f4a(mb + w.nx), FX = lds_f4a(vsub_u32(mb, w.nx) + 48u);
     const float4 NY = lds_f4a(mb + w.ny), FY = lds_f4a(vsub_u32(mb, w.ny) + 80u);
     const float4 NZ = lds_f4a(mb + w.nz), FZ = lds_f4a(vsub_u32(mb, w.nz) + 112u);
@@ -1105,7 +965,6 @@ __device__ __forceinline__ bool walk4_root(W4& w, const Stack4& S, float cull_re
     visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
     advance4(w, S, cull_rel, node_mask);
     return w.node != kNone || leaf4_pending(w);
-#endif
 }
 
 // Exact walk for the rare rays the fast path does not take (outside the Markstein

@@ -107,6 +107,8 @@ void add_stats(pt_stats* sum, const pt_stats& s)
     sum->shade_cycles += s.shade_cycles;
     sum->spill_entries += s.spill_entries;
     sum->lds_node_tests += s.lds_node_tests;
+    sum->work_units += s.work_units;
+    sum->split_pixels += s.split_pixels;
 }
 
 }  // namespace

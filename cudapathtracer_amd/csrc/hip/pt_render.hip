@@ -70,7 +70,7 @@ struct Args {
     uint32_t unit_queues;           // wavefront kernel: units dealt from kQueues counters (> 1) or one
     uint32_t tile_fast4;            // tile kernel: trace with the render-path BVH4 walk (winner check, exact
                                     // slow walk as fallback) instead of the reference-BVH culled walk
-    const DNodeW* nodes4;           // render-path BVH4 (collapsed SAH BVH; 8 wide in PT_WIDE8 builds)
+    const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
     const RNode* wbox;              // per render-path slot: its triangle's reference parent node (left/right
@@ -2108,7 +2108,7 @@ __device__ __forceinline__ void wf_main(const Args& a)
             if (state == ST_TRACE) {
                 // (the culling factor as the literal it always is: a kernel argument here was a scalar
                 // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
-                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk && !kWide8>(
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk>(
                     w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
@@ -2457,7 +2457,7 @@ struct pt_ctx {
     uint32_t top_nodes = 0;         // nodes of this scene's BVH4 that are LDS-staged (<= wf_top)
     uint32_t n4 = 0;                // nodes of this scene's BVH4
     bool wf_lds_tree = true;        // (PT_WF_LDS_TREE)
-    DNodeW* nodes4 = nullptr;
+    DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
     RNode* wbox = nullptr;
@@ -2685,7 +2685,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (const char* e = getenv("PT_WF_TOP")) c->wf_top = std::min<uint32_t>((uint32_t)std::max(0, atoi(e)), kTopNodesMax);
     }
     // render-path BVH4 (accel_build.cpp): binned SAH binary BVH collapsed to 4 wide
-    std::vector<DNodeW> an;
+    std::vector<DNode4> an;
     std::vector<DTri> at;
     if (nt == 0) {   // spheres only: no triangle structures (kernels skip the walk)
         for (int q = 0; q < 3; ++q) { c->acc_root[q] = INFINITY; c->acc_root[3 + q] = -INFINITY; }
@@ -2693,22 +2693,13 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         c->node4_mask = 1u;
     } else {
         pt::AccelBvh acc;
-#ifdef PT_WIDE8
-        constexpr int kW = 8;
-        pt::Accel8 acc4;
-#else
         constexpr int kW = 4;
         pt::Accel4 acc4;
-#endif
         lap("reference-BVH records");
         int rc4 = pt::build_accel(*sc, &acc);
         lap("SAH BVH build");
         if (timing && rc4 == PT_OK) fprintf(stderr, "pt_create: render BVH SAH cost %.6g\n", pt::accel_sah_cost(acc));
-#ifdef PT_WIDE8
-        if (rc4 == PT_OK) rc4 = pt::collapse_accel8(acc, &acc4);
-#else
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
-#endif
         lap("BVH4 collapse");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }
         // Node order: the kTopNodesMax nodes most likely to be visited first (best-first by box
@@ -2770,7 +2761,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
                 if (is_leaf(x.child[k])) {
                     const uint32_t first = (uint32_t)slot_leaf.size() - base, cnt = pt::accel_leaf_count(x.child[k]);
                     for (uint32_t j = 0; j < cnt; ++j) slot_leaf.push_back(pt::accel_leaf_slot(x.child[k]) + j);
-                    static_assert(pt::kAccel4LeafTris <= kLeafBits && pt::kAccel8LeafTris <= kLeafBits, "leaf slot mask width");
+                    static_assert(pt::kAccel4LeafTris <= kLeafBits, "leaf slot mask width");
                     if (first + cnt > kLeafBits || base >= (1u << (31 - kLeafBits))) {
                         delete c;
                         return bail(pt::fail(PT_E_SCENE, "pt_create: %u triangles exceed the render path's leaf slot range", nt));
@@ -2780,49 +2771,6 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             }
             for (int k = 0; k < kW; ++k)
                 if (x.child[k] != pt::kAccel4Empty && !(x.child[k] & PT_BVH_LEAF_FLAG)) x.child[k] = new_of[x.child[k]];
-#ifdef PT_WIDE8
-            {   // quantize: per axis the origin (lowest child plane) and the least power-of-two step with
-                // 255 steps >= the extent; planes rounded outward to the grid; empty slots inverted
-                uint32_t q[3][2][8];
-                float org[3];
-                uint32_t ebytes = 0;
-                for (int ax = 0; ax < 3; ++ax) {
-                    float lo = INFINITY, hi = -INFINITY;
-                    for (int k = 0; k < kW; ++k)
-                        if (x.child[k] != pt::kAccel4Empty) { lo = std::fmin(lo, x.lo[ax][k]); hi = std::fmax(hi, x.hi[ax][k]); }
-                    const double ext = (double)hi - (double)lo;
-                    int e = -60;
-                    if (ext > 0.0) e = std::max(-60, (int)std::ceil(std::log2(ext / 255.0)));
-                    while (std::ldexp(255.0, e) < ext) ++e;
-                    org[ax] = lo;
-                    ebytes |= (uint32_t)(e + 128) << (8 * ax);
-                    for (int k = 0; k < kW; ++k) {
-                        if (x.child[k] == pt::kAccel4Empty) { q[ax][0][k] = 255u; q[ax][1][k] = 0u; continue; }
-                        const double a = std::floor(std::ldexp((double)x.lo[ax][k] - (double)lo, -e));
-                        const double b = std::ceil(std::ldexp((double)x.hi[ax][k] - (double)lo, -e));
-                        if (!(a >= 0.0 && b <= 255.0 && a <= b)) {
-                            delete c;
-                            return bail(pt::fail(PT_E_SCENE, "pt_create: 8-wide node quantization out of range"));
-                        }
-                        q[ax][0][k] = (uint32_t)a;
-                        q[ax][1][k] = (uint32_t)b;
-                    }
-                }
-                auto pack4 = [](const uint32_t* b) { return b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24; };
-                float ebf;
-                memcpy(&ebf, &ebytes, 4);
-                an[i].hdr = make_float4(org[0], org[1], org[2], ebf);
-                uint4* qa[3] = {&an[i].qx, &an[i].qy, &an[i].qz};
-                for (int ax = 0; ax < 3; ++ax)
-                    *qa[ax] = make_uint4(pack4(q[ax][0]), pack4(q[ax][0] + 4), pack4(q[ax][1]), pack4(q[ax][1] + 4));
-                uint32_t cw[kW];
-                for (int k = 0; k < kW; ++k)   // an empty slot's word: a leaf of empty mask at the node's base
-                    cw[k] = (x.child[k] == pt::kAccel4Empty) ? (PT_BVH_LEAF_FLAG | (base << kLeafBits)) : x.child[k];
-                an[i].c0 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-                an[i].c1 = make_uint4(cw[4], cw[5], cw[6], cw[7]);
-                an[i].pad[0] = an[i].pad[1] = make_uint4(0u, 0u, 0u, 0u);
-            }
-#else
             an[i].lox = make_float4(x.lo[0][0], x.lo[0][1], x.lo[0][2], x.lo[0][3]);
             an[i].loy = make_float4(x.lo[1][0], x.lo[1][1], x.lo[1][2], x.lo[1][3]);
             an[i].loz = make_float4(x.lo[2][0], x.lo[2][1], x.lo[2][2], x.lo[2][3]);
@@ -2831,7 +2779,6 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             an[i].hiz = make_float4(x.hi[2][0], x.hi[2][1], x.hi[2][2], x.hi[2][3]);
             an[i].child = make_uint4(x.child[0], x.child[1], x.child[2], x.child[3]);
             an[i].pad = make_uint4(0u, 0u, 0u, 0u);
-#endif
         }
         if (slot_leaf.size() != nt) { delete c; return bail(pt::fail(PT_E_SCENE, "pt_create: BVH4 reaches %zu of %u triangles", slot_leaf.size(), nt)); }
         at.resize(nt);
@@ -3056,6 +3003,17 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     for (const int32_t v : {p->tile_w, p->tile_h})
         if (v != 0 && (v < 8 || v > 256 || v % 8 != 0))
             return pt::fail(PT_E_INVALID, "pt_render: tile size %dx%d (0 = 8, else multiples of 8 up to 256)", p->tile_w, p->tile_h);
+    // the per-triangle counts live in one context-wide buffer (pt_tri_counts reads it back): only one render
+    // in flight may fill them
+    if ((p->flags & PT_FLAG_COUNT) && (p->flags & PT_FLAG_TRI_COUNTS) && c->fl_n > 0)
+        return pt::fail(PT_E_INVALID, "pt_render_device_async: PT_FLAG_TRI_COUNTS while a render is in flight");
+    {   // the padded tile grid (tiles x tile_w x tile_h slots) must fit the kernels' 32-bit unit indices
+        const uint64_t tw64 = p->tile_w ? (uint64_t)p->tile_w : 8u, th64 = p->tile_h ? (uint64_t)p->tile_h : 8u;
+        const uint64_t slots = (((uint64_t)p->width + tw64 - 1) / tw64) * (((uint64_t)p->height + th64 - 1) / th64) * tw64 * th64;
+        if (slots > 0xffffffffull)
+            return pt::fail(PT_E_INVALID, "pt_render: %dx%d in %llux%llu tiles pads to %llu pixel slots (limit 2^32-1)",
+                            p->width, p->height, (unsigned long long)tw64, (unsigned long long)th64, (unsigned long long)slots);
+    }
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
     // this render's slot: its events and its buffer set.  The slot's previous render was collected by
@@ -3139,6 +3097,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     a.tile_fast4 = (!refwalk && !(p->flags & PT_FLAG_REFERENCE_BVH) && near_cam && c->tile_fast4 && c->num_tris > 0) ? 1u : 0u;
     HIP_TRY(hipEventRecord(F.ev0, stream));
     bool kernel_events = false;   // ek0/ek1 recorded around the integration kernel (wavefront path)
+    bool seeded_now = false;      // seed_table enqueued for p->seed by this render
     uint64_t units = 0, split = 0;
     if (p->spp > 0 && a.ntiles_shard > 0 && wavefront) {
         // 4 waves per block; per wave an LDS ring of kRing packed entries x 64 lanes, deeper
@@ -3314,9 +3273,12 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
                 B.seed_valid = false;
             }
             if (!B.seed_valid || B.seed_cached != p->seed) {   // (depends on the seed only: kept across renders)
+                // (marked valid only once the whole render is enqueued: any error return below leaves the
+                // slot unseeded, so the next render seeds again instead of trusting a table never written)
+                B.seed_valid = false;
                 hipLaunchKernelGGL(seed_table, dim3(1), dim3(256), 0, stream, b, B.seed_states);
-                B.seed_cached = p->seed;
-                B.seed_valid = true;
+                HIP_TRY(hipGetLastError());
+                seeded_now = true;
             }
             b.jump_bytes = c->jump_bytes;
             b.seed_states = B.seed_states;
@@ -3379,6 +3341,10 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     F.split = split;
     F.spp = p->spp;
     F.bounces = p->bounces;
+    if (seeded_now) {
+        B.seed_cached = p->seed;
+        B.seed_valid = true;
+    }
     ++c->fl_n;
     return PT_OK;
 }
@@ -3520,11 +3486,7 @@ int pt_render(pt_ctx* c, const pt_params* p, const pt_camera* cam, float* out_rg
 
 static size_t stack_words_per_lane(const pt_ctx* c)
 {
-#ifdef PT_WIDE8
-    size_t per_lane = (size_t)(7 * c->acc4_depth + 4);   // (an 8-wide visit pushes at most 7 entries)
-#else
     size_t per_lane = (size_t)(3 * c->acc4_depth + 4);
-#endif
     if (per_lane < (size_t)(2 * (c->depth + 2))) per_lane = (size_t)(2 * (c->depth + 2));
     return per_lane;
 }
@@ -3671,6 +3633,8 @@ extern "C" int pt_shard_pixels(int w, int h, int shard_index, int shard_count, i
     m.tile_blocks = m.tile_bx * (m.tile_h / kTile);
     const uint32_t nts = (ntiles > (uint32_t)shard_index) ? (ntiles - (uint32_t)shard_index + (uint32_t)shard_count - 1) / (uint32_t)shard_count : 0u;
     const uint64_t slots = (uint64_t)nts * m.tile_w * m.tile_h;
+    if ((uint64_t)(((uint32_t)h + m.tile_h - 1) / m.tile_h) * m.tiles_x * m.tile_w * m.tile_h > 0xffffffffull)
+        return pt::fail(PT_E_INVALID, "pt_shard_pixels: %dx%d pads to more than 2^32-1 pixel slots", w, h);
     uint32_t n = 0;
     for (uint64_t q = 0; q < slots; ++q) {
         uint32_t px, py;

@@ -318,7 +318,7 @@ float area_of(const float* b)
     return surface(b, b + 3);
 }
 
-// W-wide collapse (W = 4: Accel4; W = 8: Accel8), at most kTris triangles in a node's leaf children
+// W-wide collapse (W = 4: Accel4), at most kTris triangles in a node's leaf children
 template <int W, uint32_t kTris, class Node, class Out>
 struct Collapser {
     const AccelBvh& bin;
@@ -391,17 +391,6 @@ int collapse_accel4(const AccelBvh& bin, Accel4* out)
     Collapser<4, kAccel4LeafTris, Accel4Node, Accel4> col{bin, *out};
     const uint32_t root = col.run(0, 0);
     if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
-    out->depth = col.max_depth;
-    return PT_OK;
-}
-
-int collapse_accel8(const AccelBvh& bin, Accel8* out)
-{
-    out->nodes.clear();
-    out->nodes.reserve(bin.nodes.size() / 3 + 1);
-    Collapser<8, kAccel8LeafTris, Accel8Node, Accel8> col{bin, *out};
-    const uint32_t root = col.run(0, 0);
-    if (root != 0) return fail(PT_E_SCENE, "collapse_accel8: internal error");
     out->depth = col.max_depth;
     return PT_OK;
 }

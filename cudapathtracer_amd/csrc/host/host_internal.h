@@ -114,18 +114,6 @@ struct Accel4 {
     int depth = 0;
 };
 int collapse_accel4(const AccelBvh& bin, Accel4* out);
-// 8-wide collapse (the same rule, at most kAccel8LeafTris triangles in a node's leaf children): the
-// render path's 8-wide quantized nodes (pt_render.hip, PT_WIDE8 builds)
-constexpr uint32_t kAccel8LeafTris = 8;
-struct Accel8Node {
-    float lo[3][8], hi[3][8];   // [axis][child]
-    uint32_t child[8];          // inner node index, PT_BVH_LEAF_FLAG | slot, or kAccel4Empty
-};
-struct Accel8 {
-    std::vector<Accel8Node> nodes;
-    int depth = 0;
-};
-int collapse_accel8(const AccelBvh& bin, Accel8* out);
 
 // ---- BVH (BVH.h) ------------------------------------------------------------------------
 int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,

@@ -54,15 +54,21 @@ class OCounters(C.Structure):
                 ("tri_counts", C.c_void_p)]
 
 
-_lib = None
+_libs = {}
+# sensitivity variants of the restatement (oracle/Makefile VARIANTS; tools/parity/ref_gap.py)
+VARIANTS = ("fma", "fma_notri", "libm", "ulp1", "ulp2", "unfused", "nvcc")
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def lib(variant=None):
+    """The oracle library; variant = one of VARIANTS loads that sensitivity build instead (same ABI)."""
+    h = _libs.get(variant)
+    if h is None:
+        path = LIB if variant is None else os.path.join(HERE, "variants", "liboracle_%s.so" % variant)
+        if variant is not None and variant not in VARIANTS:
+            raise ValueError("unknown oracle variant %r" % (variant,))
+        if not os.path.exists(path):
             build()
-        h = C.CDLL(LIB)
+        h = C.CDLL(path)
         h.or_xorwow_step_images.argtypes = [C.c_void_p]
         h.or_xorwow_jump_images.argtypes = [C.c_int, C.c_void_p]
         h.or_xorwow_init.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(OXorwow)]
@@ -91,8 +97,8 @@ def lib():
         h.or_render.restype = C.c_int
         h.or_write_ppm_imgbuf.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
         h.or_write_ppm_imgbuf.restype = C.c_int
-        _lib = h
-    return _lib
+        _libs[variant] = h
+    return h
 
 
 class OracleScene:
@@ -127,10 +133,10 @@ def camera(pos, dist_from_film, focal_length, radius, width, height):
 
 
 def render(scene: OracleScene, cam: OCamera, width, height, spp, bounces=3, integrator=0, seed=1234, pixels=None,
-           threads=0, tri_counts=None):
+           threads=0, tri_counts=None, variant=None):
     """f64 mean image (H, W, 3); pixels = iterable of y*W+x (default: all).  Returns (img, counters).
     tri_counts: optional uint32[num_tris] array the per-triangle test counts are added to
-    (kernel.cu:133 test[k] += 1)."""
+    (kernel.cu:133 test[k] += 1).  variant: a sensitivity build (VARIANTS) instead of the oracle."""
     if pixels is None:
         pixels = np.arange(width * height, dtype=np.uint32)
     pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
@@ -139,7 +145,7 @@ def render(scene: OracleScene, cam: OCamera, width, height, spp, bounces=3, inte
     if tri_counts is not None:
         assert tri_counts.dtype == np.uint32 and tri_counts.flags.c_contiguous and len(tri_counts) == scene.c.num_tris
         cnt.tri_counts = tri_counts.ctypes.data
-    rc = lib().or_render(C.byref(scene.c), C.byref(cam), width, height, spp, bounces, integrator, seed,
+    rc = lib(variant).or_render(C.byref(scene.c), C.byref(cam), width, height, spp, bounces, integrator, seed,
                          pixels.ctypes.data, len(pixels), threads, out.ctypes.data, C.byref(cnt))
     if rc != 0:
         raise RuntimeError("or_render failed: %d" % rc)

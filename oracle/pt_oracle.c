@@ -157,19 +157,49 @@ uint32_t or_xorwow_next(or_xorwow* st)
     return st->v[4] + st->d;
 }
 
-/* curand_uniform (kernel.cu:58): x * CURAND_2POW32_INV + CURAND_2POW32_INV/2, contracted. */
+/* curand_uniform (kernel.cu:58): x * CURAND_2POW32_INV + CURAND_2POW32_INV/2, contracted.
+ * OR_UNIFORM_UNFUSED (sensitivity variant, tools/parity/ref_gap.py): the same expression rounded
+ * twice, as a build without FMA contraction would evaluate it. */
 float or_uniform(or_xorwow* st)
 {
     uint32_t x = or_xorwow_next(st);
+#ifdef OR_UNIFORM_UNFUSED
+    volatile float p = (float)x * 2.3283064e-10f;   /* (volatile: no contraction in any build) */
+    return p + 2.3283064e-10f / 2.0f;
+#else
     return fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+#endif
 }
 
 /* ---------------------------------------------------------------- sin/cos */
+/* Sensitivity variants (tools/parity/ref_gap.py; the default build defines neither):
+ *   OR_SINCOS_LIBM       glibc sinf/cosf instead of det_sincos;
+ *   OR_SINCOS_PERTURB=k  det_sincos's results moved by a pseudo-random j ulp, |j| <= k, chosen by a
+ *                        hash of the argument's bits -- CUDA documents sinf/cosf to within 2 ulp, so
+ *                        k = 2 is the worst case the reference's device library allows. */
+#ifdef OR_SINCOS_PERTURB
+static float ulp_move(float v, uint32_t h)
+{
+    int j = (int)(h % (2u * OR_SINCOS_PERTURB + 1u)) - OR_SINCOS_PERTURB;
+    for (; j > 0; --j) v = nextafterf(v, INFINITY);
+    for (; j < 0; ++j) v = nextafterf(v, -INFINITY);
+    return v;
+}
+#endif
+
 /* Deterministic float sin/cos for the sampling angles (kernel.cu:65-68, 84-88; camera.h:85-87):
  * double-precision Cody-Waite reduction by pi/2 and Taylor polynomials to degree 17/18, rounded
- * once to float.  Plain IEEE double ops in a fixed order, so gfx950 reproduces it exactly. */
+ * once to float.  Plain IEEE double ops in a fixed order, so gfx950 reproduces it exactly.
+ * (Never contracted, whatever the build's -ffp-contract: the FMA-contraction variant of
+ * ref_gap.py contracts the reference's own expressions, not this function's stand-in for cosf.) */
+__attribute__((optimize("fp-contract=off")))
 void or_sincos(float theta, float* s_out, float* c_out)
 {
+#ifdef OR_SINCOS_LIBM
+    *s_out = sinf(theta);
+    *c_out = cosf(theta);
+    return;
+#endif
     const double x = (double)theta;
     const double two_over_pi = 0.63661977236758138;
     const double pio2_hi = 1.5707963267948966;
@@ -206,10 +236,23 @@ void or_sincos(float theta, float* s_out, float* c_out)
     }
     *s_out = (float)sv;
     *c_out = (float)cv;
+#ifdef OR_SINCOS_PERTURB
+    {
+        uint32_t b;
+        memcpy(&b, &theta, 4);
+        const uint32_t h = b * 0x9e3779b1u;
+        *s_out = ulp_move(*s_out, h >> 7);
+        *c_out = ulp_move(*c_out, (h ^ 0x5bd1e995u) * 0x85ebca6bu >> 9);
+    }
+#endif
 }
 
 /* -------------------------------------------------------------- geometry */
-/* modelLoader.h:49-83 triIntersect */
+/* modelLoader.h:49-83 triIntersect.  (OR_TRI_NO_CONTRACT: the fma_notri sensitivity variant keeps this one
+ * function uncontracted while the rest of the build contracts, tools/parity/ref_gap.py) */
+#ifdef OR_TRI_NO_CONTRACT
+__attribute__((optimize("fp-contract=off")))
+#endif
 float or_tri_intersect(or_vec3 o, or_vec3 ray, const or_vec3* verts, const or_tri* t)
 {
     or_vec3 v0 = verts[t->v0], v1 = verts[t->v1], v2 = verts[t->v2];

@@ -397,6 +397,8 @@ def test_group_render_one_device_equals_render(cb):
     assert np.array_equal(img2.view(np.uint32), ref.view(np.uint32))
     assert gst["samples"] == st["samples"] == w * h * spp
     assert gst["rays_nominal"] == st["rays_nominal"] == w * h * spp * 4
+    assert gst["work_units"] == st["work_units"] > 0
+    assert gst["split_pixels"] == st["split_pixels"]
     with pt.Renderer(s, 0) as r2:
         with pytest.raises(pt.PtError) as e:
             pt.Group([r, r2])
@@ -512,6 +514,14 @@ def test_async_renders_queue_back_to_back(cb):
     # the pixel's chunk 0 has not yet published it (a race of timing, not of results)
     for x, y in ((sa, st0), (sb, st1)):
         assert 0 < x["rays_traced"] <= x["rays_reference"] and abs(x["rays_traced"] - y["rays_traced"]) <= x["samples"]
+    # the per-triangle counts are one context-wide buffer: a render filling them is refused while
+    # another render is in flight
+    r.render_device_async(cam, a.data_ptr(), w, h, spp, bounces=3, stream_ptr=stream)
+    with pytest.raises(pt.PtError) as e:
+        r.render_device_async(cam, b.data_ptr(), w, h, spp, bounces=3, stream_ptr=stream,
+                              flags=pt.PT_FLAG_COUNT | pt.PT_FLAG_TRI_COUNTS)
+    assert e.value.code == pt.PT_E_INVALID
+    r.wait()
 
 
 @pytest.mark.gpu

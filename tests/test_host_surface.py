@@ -165,6 +165,10 @@ def test_morton_framebuffer_ppm_matches_reference_loop(tmp_path):
             pt.write_ppm(str(tmp_path / "bad.ppm"), np.zeros((bw * bh, 3), np.float32), pixel_order=pt.PT_ORDER_MORTON,
                          width=bw, height=bh)
         assert e.value.code == pt.PT_E_INVALID
+    # the buffer must hold width*height*3 values (the C loop reads rgb[morton(x,y)*3 ..]): checked before the call
+    for bad_buf, bw, bh in ((buf[: w * h // 2], w, h), (buf, None, h), (buf, w, None), (buf, 2 * w, 2 * h)):
+        with pytest.raises(ValueError):
+            pt.write_ppm(str(tmp_path / "bad.ppm"), bad_buf, pixel_order=pt.PT_ORDER_MORTON, width=bw, height=bh)
 
 
 def test_shard_tiles_partition_the_image():
