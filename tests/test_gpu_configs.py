@@ -224,3 +224,21 @@ def test_merged_shading_records_bit_identical(standin, monkeypatch):
     with pt.Renderer(s, 0) as r2:
         b, _ = r2.render(cam, w, h, spp, bounces=5)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_c3_full_frame_repeatable(standin):
+    """The full C3 frame is the same bits on every render, for both integrators: nothing the persistent
+    kernel shares between lanes (unit counters, the published primary-hit words of split pixels, the
+    LDS queues) may change a result, only which lane computes it.  (Round 3's full-precision 8-wide
+    experiment once failed the integrator-1 full-frame comparison and did not on re-running the same
+    build, profiles/r04_w8f: this checks the product for run-to-run differences directly.)"""
+    s, r = standin
+    w, h, spp = 1920, 1080, 256
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    for integ in (0, 1):
+        a, _ = r.render(cam, w, h, spp, bounces=3, integrator=integ)
+        b, _ = r.render(cam, w, h, spp, bounces=3, integrator=integ)
+        with pt.Renderer(s, 0) as r2:   # a fresh context: fresh buffers and seed tables
+            c, _ = r2.render(cam, w, h, spp, bounces=3, integrator=integ)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), integ
+        assert np.array_equal(a.view(np.uint32), c.view(np.uint32)), integ

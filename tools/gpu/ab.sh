@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of bench configurations (GPU box, repo root).
 #   CONFIGS="label:VAR=VAL,VAR2=VAL2 label2: ..."  (an empty env = the in-tree library, defaults)
-#   TEST=1: smoke + the GPU suite first (in-tree library); ROUNDS (default 2) alternations;
+#   TEST=1: smoke + the GPU suite first (in-tree library; TESTENV="VAR=VAL,..." for the suite); ROUNDS (default 2);
 #   BENCH_ARGS: extra bench.py arguments (e.g. --config C2); STEPS (default 4).
 set -o pipefail
 export TMPDIR=/tmp
@@ -10,7 +10,7 @@ mkdir -p $OUT
 if [ -n "$TEST" ]; then
   timeout -k 10 300 python3 __graft_entry__.py smoke > $OUT/smoke.log 2>&1 || { echo smoke-fail > $OUT/done.txt; tail -20 $OUT/smoke.log; exit 1; }
   echo "smoke ok"
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:+-k "$TESTS"} \
+  timeout -k 10 900 env ${TESTENV//,/ } python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:+-k "$TESTS"} \
       > $OUT/pytest_gpu.log 2>&1 || { echo pytest-fail > $OUT/done.txt; tail -40 $OUT/pytest_gpu.log; exit 1; }
   tail -1 $OUT/pytest_gpu.log
 fi
