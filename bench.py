@@ -200,6 +200,24 @@ def roofline(counts, kms, W, H, args, world):
     return roof
 
 
+L1_LINES_PER_CU_CYCLE = 1.0   # measured ceiling: tools/gpu/micro/node_gather.hip, profiles/r04_l1_lookups
+
+
+def l1_roofline(roof):
+    """The walk's binding resource (profiles/r04_l1_lookups): the L1's cache-line lookups.  A
+    scattered dwordx4 costs one lookup per lane (per distinct 128-B line), a node visit seven; a dependent
+    gather loop of them runs at ~1 line per CU-cycle however the lines are spread over L2 / Infinity Cache /
+    HBM (10 and 100 MB tables alike) and however many lanes are masked or out of range.  achieved = the
+    render kernel's TCP_TOTAL_CACHE_ACCESSES per CU-cycle from the same profile as `roofline`."""
+    b = (roof or {}).get("binding") or {}
+    x = b.get("l1_lookups_per_cu_cycle")
+    if x is None:
+        return None
+    return {"bound": "l1_lookups", "achieved": x, "peak": L1_LINES_PER_CU_CYCLE, "unit": "lines/CU-cycle",
+            "frac": round(x / L1_LINES_PER_CU_CYCLE, 4), "source": (roof.get("traffic_source") or {}).get("profile"),
+            "peak_source": "tools/gpu/micro/node_gather.hip (profiles/r04_l1_lookups)"}
+
+
 def cache_roofline(counts, kms):
     """The algorithmic bytes (records the walk and the shading pass request: node records not served by
     the LDS top, triangle records, per-ray shading reads, output) over the kernel time, against the L2
@@ -465,6 +483,7 @@ def main():
             "image_finite": finite,
             "roofline": roof,
             "cache_roofline": cache_roofline(dict(counts, spp=args.spp), kms) if counts is not None else None,
+            "l1_roofline": l1_roofline(roof),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
