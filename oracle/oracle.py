@@ -82,6 +82,8 @@ def lib(variant=None):
         h.or_trace_batch_counts.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         h.or_trace_batch_counts.restype = C.c_int
         h.or_tri_intersect.argtypes = [OVec3, OVec3, C.c_void_p, C.c_void_p]
+        h.or_get_tangent.argtypes = [OVec3, C.POINTER(OVec3)]
+        h.or_brdf.argtypes = [C.c_void_p, C.c_void_p]
         h.or_tri_intersect.restype = C.c_float
         h.or_ray_aabb.argtypes = [OVec3, OVec3, OVec3, OVec3]
         h.or_ray_aabb.restype = C.c_int
@@ -194,6 +196,25 @@ def jump_images(log2_steps):
     img = np.zeros(800, dtype=np.uint32)
     lib().or_xorwow_jump_images(log2_steps, img.ctypes.data)
     return img
+
+
+def helpers(normals, albedos, variant=None):
+    """kernel.cu:44-54 getTangent of each normal (f32 (n, 3)) and :101-104 BRDF of each albedo (f64 (n, 3)),
+    as the restatement computes them."""
+    L = lib(variant)
+    nrm = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+    alb = np.ascontiguousarray(albedos, dtype=np.float64).reshape(-1, 3)
+    tan = np.empty_like(nrm)
+    brdf = np.empty_like(alb)
+    t = OVec3()
+    out = np.empty(3, dtype=np.float64)
+    for i in range(len(nrm)):
+        L.or_get_tangent(OVec3(*nrm[i]), C.byref(t))
+        tan[i] = (t.x, t.y, t.z)
+    for i in range(len(alb)):
+        L.or_brdf(alb[i].ctypes.data, out.ctypes.data)
+        brdf[i] = out
+    return tan, brdf
 
 
 def refgen_available():

@@ -474,6 +474,17 @@ static or_vec3 cosine_ray(or_vec3 n, or_xorwow* rng)                   /* kernel
 }
 static col brdf(const or_mat* m) { return cmulf(mat_albedo(m), (float)(1 / 3.14159)); }  /* kernel.cu:101-104 */
 
+/* exported for the golden checks of getTangent / BRDF against the reference's own code (refgen helpers) */
+void or_get_tangent(or_vec3 n, or_vec3* out) { *out = get_tangent(n); }
+void or_brdf(const double albedo[3], double out[3])
+{
+    or_mat m;
+    memset(&m, 0, sizeof(m));
+    m.albedo[0] = albedo[0]; m.albedo[1] = albedo[1]; m.albedo[2] = albedo[2];
+    const col c = brdf(&m);
+    out[0] = c.r; out[1] = c.g; out[2] = c.b;
+}
+
 /* Area-CDF light pick + uniform point (kernel.cu:466-495, 231-262).  Returns the chosen
  * primitive id; a triangle gives p = v0 + a1*u + a2*v.  Sphere lights (d8 policy) enter the
  * CDF with area 4*3.14159*r^2 and give the uniform point c + r*(sqrt(1-z^2)cos(phi),

@@ -118,6 +118,10 @@ int      or_render(const or_scene* sc, const or_camera* cam, int width, int heig
  * Returns 0, or -1 when the file cannot be written. */
 int      or_write_ppm_imgbuf(const char* path, const double* imgbuf, int width, int height);
 
+/* kernel.cu:44-54 getTangent, :101-104 BRDF (the restatement's, exported for golden checks) */
+void or_get_tangent(or_vec3 n, or_vec3* out);
+void or_brdf(const double albedo[3], double out[3]);
+
 #ifdef __cplusplus
 }
 #endif

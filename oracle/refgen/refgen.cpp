@@ -27,6 +27,9 @@
 //                scene's buildBVH() array; counts: numTris x u32, the trace()'s test[] increments summed
 //                over all rays (kernel.cu:133; sized numTris here -- the reference's buffer has
 //                bvh.size = numTris-1 entries, kernel.cu:696, so its last increment lands out of bounds)
+//   refgen helpers <in.bin> <out.bin> in: n x {normal[3] f32, pad f32, albedo[3] f64}; out: n x {getTangent(normal)[3]
+//                f32, pad, BRDF(albedo)[3] f64} -- kernel.cu:44-54 and :101-104, extracted verbatim into
+//                oracle/_ref/ref_helpers.inc by oracle/Makefile
 //   refgen ppm   <imgbuf.bin> <W> <H>  (writes ./image.ppm, as the reference does)
 //                in: W*H x 3 f64, the reference's imgBuffer_host (Morton-indexed: kernel.cu:543,552); the
 //                PPM is written by the reference's own output loop (kernel.cu:763-778, "save the file"),
@@ -49,6 +52,9 @@ using std::abs;
 #include "/root/reference/modelLoader.h"
 #include "/root/reference/BVH.h"
 #include "/root/reference/camera.h"
+#ifdef REFGEN_HELPERS
+#include REFGEN_HELPERS    // kernel.cu:44-54 getTangent and :101-104 BRDF, extracted verbatim by oracle/Makefile
+#endif
 #ifdef REFGEN_TRACE
 #define MAX_BVH_DEPTH 64   // kernel.cu:35
 #include REFGEN_TRACE      // kernel.cu:107-161, extracted verbatim by oracle/Makefile
@@ -212,6 +218,30 @@ int main(int argc, char** argv)
         }
         spit(argv[3], out.data(), out.size());
         spit(argv[4], test.data(), test.size() * 4);
+        return 0;
+    }
+#endif
+#ifdef REFGEN_HELPERS
+    if (cmd == "helpers") {
+        std::vector<char> in = slurp(argv[2]);
+        const size_t n = in.size() / 40;
+        std::vector<char> out(n * 40, 0);
+        for (size_t i = 0; i < n; ++i) {
+            float nv[3];
+            double alb[3];
+            memcpy(nv, &in[40 * i], 12);
+            memcpy(alb, &in[40 * i + 16], 24);
+            const vec3 t = getTangent(vec3(nv[0], nv[1], nv[2]));                          // kernel.cu:44
+            materialDesc m;
+            m.albedo = color(alb[0], alb[1], alb[2]);
+            m.emmision = color(0.0, 0.0, 0.0);   // (the reference's spelling, modelLoader.h:21-25)
+            const color b = BRDF(m, vec3(0, 0, 0), vec3(0, 0, 0));                         // kernel.cu:101
+            const float tv[3] = {t.x, t.y, t.z};
+            const double bv[3] = {b.r, b.g, b.b};
+            memcpy(&out[40 * i], tv, 12);
+            memcpy(&out[40 * i + 16], bv, 24);
+        }
+        spit(argv[3], out.data(), out.size());
         return 0;
     }
 #endif

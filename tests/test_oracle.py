@@ -199,3 +199,15 @@ def test_trace_equals_bruteforce_restatement():
         tri, t = oracle.trace(osc, o, d)
         assert tri == best[2]
         assert np.float32(t).tobytes() == np.float32(best[0]).tobytes()
+
+
+def test_sampling_frame_and_brdf_match_reference():
+    """getTangent (kernel.cu:44-54: the larger of n x z and n x y, strict '>' so ties take n x y) and BRDF
+    (:101-104: albedo * (1/3.14159) in double), compiled from the reference's own lines (refgen helpers,
+    extracted verbatim at build time): the restatement equals them bit for bit on random, axis-aligned,
+    tied and mesh normals and on random and material albedos.  (The rest of kernel.cu's sampling code --
+    randRay, cosineWeightedRay -- draws through cuRAND and is not built here)"""
+    g = golden("kat_helpers.npz")
+    tan, brdf = oracle.helpers(g["normal"], g["albedo"])
+    assert np.array_equal(tan.view(np.uint32), g["tangent"].astype(np.float32).view(np.uint32))
+    assert np.array_equal(brdf.view(np.uint64), g["brdf"].view(np.uint64))

@@ -178,6 +178,36 @@ def kat_morton(tmp):
     np.savez_compressed(os.path.join(GOLD, "kat_morton.npz"), xy=m[:, 0], back=m[:, 1])
 
 
+def kat_helpers(tmp, rng):
+    """getTangent (kernel.cu:44-54) and BRDF (:101-104) from the reference's own code (refgen helpers):
+    random unit normals, the axis directions of both signs, ties |n.y| == |n.z| (where getTangent's strict
+    '>' picks c2), and the fixture scenes' face normals; random albedos and the scenes' material albedos."""
+    n_rand = 4000
+    nr = rng.normal(size=(n_rand, 3))
+    nr /= np.linalg.norm(nr, axis=1, keepdims=True)
+    axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float64)
+    a = rng.uniform(0.1, 1.0, 200)
+    ties = np.stack([rng.uniform(-1, 1, 200), a, a * rng.choice([-1.0, 1.0], 200)], axis=1)
+    ties /= np.linalg.norm(ties, axis=1, keepdims=True)
+    face = [load_scene_normals(n) for n in ("cornell", "cornell_blob")]
+    nrm = np.concatenate([nr, axes, ties] + face).astype(np.float32)
+    alb = rng.uniform(0, 1, (len(nrm), 3))
+    mats = np.concatenate([np.load(os.path.join(GOLD, "scene_%s.npz" % n))["mats"]["albedo"] for n in ("cornell", "quirks")])
+    alb[: len(mats)] = mats
+    rec = np.zeros(len(nrm), dtype=[("n", "<f4", (3,)), ("pad", "<f4"), ("alb", "<f8", (3,))])
+    rec["n"] = nrm
+    rec["alb"] = alb
+    rec.tofile(os.path.join(tmp, "helpers.in"))
+    run_ref(["helpers", os.path.join(tmp, "helpers.in"), os.path.join(tmp, "helpers.out")])
+    out = np.fromfile(os.path.join(tmp, "helpers.out"), dtype=rec.dtype)
+    np.savez_compressed(os.path.join(GOLD, "kat_helpers.npz"), normal=nrm, albedo=alb, tangent=out["n"], brdf=out["alb"])
+
+
+def load_scene_normals(name):
+    tris = np.load(os.path.join(GOLD, "scene_%s.npz" % name))["tris"]
+    return np.stack([tris["nx"], tris["ny"], tris["nz"]], axis=1).astype(np.float64)
+
+
 def kat_tone(tmp, rng):
     c = np.concatenate([rng.exponential(1.0, 3000), rng.uniform(0, 1e-3, 300), [0.0, 1e-300, 1.0, 3.0, 1e6, 1e300],
                         rng.uniform(0, 20, 700)]).astype(np.float64)
@@ -283,6 +313,10 @@ def main():
         with tempfile.TemporaryDirectory() as tmp:
             kat_trace(tmp)
         return
+    if sys.argv[1:] == ["--only", "helpers"]:
+        with tempfile.TemporaryDirectory() as tmp:
+            kat_helpers(tmp, np.random.default_rng(20261017))
+        return
     if sys.argv[1:] == ["--only", "ppm"]:
         with tempfile.TemporaryDirectory() as tmp:
             kat_ppm_morton(tmp)
@@ -319,6 +353,7 @@ def main():
         kat_cam(tmp, rng)
         kat_morton(tmp)
         kat_tone(tmp, rng)
+        kat_helpers(tmp, rng)
         kat_trace(tmp)
         kat_ppm_morton(tmp)
     xorwow_fixture()
