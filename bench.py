@@ -204,16 +204,17 @@ L1_LINES_PER_CU_CYCLE = 1.0   # measured ceiling: tools/gpu/micro/node_gather.hi
 
 
 def l1_roofline(roof):
-    """The walk's binding resource (profiles/r04_l1_lookups): the L1's cache-line lookups.  A
-    scattered dwordx4 costs one lookup per lane (per distinct 128-B line), a node visit seven; a dependent
-    gather loop of them runs at ~1 line per CU-cycle however the lines are spread over L2 / Infinity Cache /
-    HBM (10 and 100 MB tables alike) and however many lanes are masked or out of range.  achieved = the
-    render kernel's TCP_TOTAL_CACHE_ACCESSES per CU-cycle from the same profile as `roofline`."""
+    """Utilisation of the L1's cache-line lookups (profiles/r04_l1_lookups).  A scattered
+    dwordx4 costs one lookup per lane (per distinct 128-B line), a node visit seven; a dependent gather loop
+    of them runs at ~1 line per CU-cycle however the lines are spread over L2 / Infinity Cache / HBM (10 and
+    100 MB tables alike) and however many lanes are masked or out of range.  achieved = the render kernel's
+    TCP_TOTAL_CACHE_ACCESSES per CU-cycle from the same profile as `roofline`.  Not the walk's limiter: 18%
+    fewer lookups left the rate unchanged (profiles/r04_topasm); the step's serial chain is."""
     b = (roof or {}).get("binding") or {}
     x = b.get("l1_lookups_per_cu_cycle")
     if x is None:
         return None
-    return {"bound": "l1_lookups", "achieved": x, "peak": L1_LINES_PER_CU_CYCLE, "unit": "lines/CU-cycle",
+    return {"bound": "l1_lookups", "binding": False, "achieved": x, "peak": L1_LINES_PER_CU_CYCLE, "unit": "lines/CU-cycle",
             "frac": round(x / L1_LINES_PER_CU_CYCLE, 4), "source": (roof.get("traffic_source") or {}).get("profile"),
             "peak_source": "tools/gpu/micro/node_gather.hip (profiles/r04_l1_lookups)"}
 
