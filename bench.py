@@ -41,7 +41,7 @@ TRI_BYTES = 48            # one triangle record {v0, e1, e2, id, rank, parent}
 # the sources that define the render kernel: profiles/traffic.json is used only when it was measured
 # on a build of exactly these (a stale PMC number cannot ride along)
 KERNEL_SOURCES = ("cudapathtracer_amd/csrc/hip/pt_render.hip", "cudapathtracer_amd/csrc/hip/pt_device.h",
-                  "cudapathtracer_amd/csrc/Makefile")
+                  "cudapathtracer_amd/csrc/Makefile", "cudapathtracer_amd/csrc/host/accel_build.cpp")
 
 
 def kernel_source_sha256():

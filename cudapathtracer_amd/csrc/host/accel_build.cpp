@@ -382,17 +382,157 @@ struct Collapser {
     }
 };
 
+// SAH-optimal 4-wide collapse by dynamic programming over the binary tree (the wide-BVH
+// conversion of Ylitie et al. 2017 for W = 4): every binary inner node x gets the least cost of
+// standing for its subtree in at most m = 1..4 slots of a wide node, where a slot is
+//   a leaf (a binary leaf, or an inner node of <= kAccelLeafMax triangles merged into one):
+//     c_tri * area * triangles, or
+//   a wide node of its own: c_node * area + the best spread of x's two children over 4 slots,
+// and m >= 2 may instead pass x's two children on (one slot each or more, split m between them).
+// Leaves of <= 2 triangles in <= 4 slots keep a node's leaf triangles within kAccel4LeafTris.
+struct DpCollapser {
+    const AccelBvh& bin;
+    Accel4& out;
+    float cn, ct;
+    int max_depth = 0;
+    struct Rec {
+        float area = 0.0f;
+        const float* box = nullptr;   // the node's box as its parent holds it (root: root_box)
+        uint32_t tris = 0;
+        bool as_leaf = false;         // a single slot for it is a merged leaf (else its own wide node)
+        float E[5];                   // E[m]: the subtree in <= m slots
+        bool self[5];                 // E[m] takes one slot for the node itself
+        int8_t split[5];              // passing on: slots for the left child (the right gets the rest)
+    };
+    std::vector<Rec> rec;
+
+    float leaf_cost(uint32_t ref, const float* box) const { return ct * area_of(box) * (float)accel_leaf_count(ref); }
+    float E(uint32_t ref, const float* box, int m) const
+    {
+        return (ref & PT_BVH_LEAF_FLAG) ? leaf_cost(ref, box) : rec[ref].E[m];
+    }
+    uint32_t tris_of(uint32_t ref) const { return (ref & PT_BVH_LEAF_FLAG) ? accel_leaf_count(ref) : rec[ref].tris; }
+
+    void solve()
+    {
+        const size_t n = bin.nodes.size();
+        rec.assign(n, Rec());
+        rec[0].box = bin.root_box;
+        for (size_t i = 0; i < n; ++i)   // preorder: a parent comes before its children
+            for (int k = 0; k < 2; ++k)
+                if (!(bin.nodes[i].child[k] & PT_BVH_LEAF_FLAG)) rec[bin.nodes[i].child[k]].box = bin.nodes[i].box[k];
+        for (size_t i = n; i-- > 0;) {   // reverse preorder: children first
+            const AccelNode& x = bin.nodes[i];
+            Rec& r = rec[i];
+            r.area = area_of(r.box);
+            r.tris = tris_of(x.child[0]) + tris_of(x.child[1]);
+            float D[5] = {INFINITY, INFINITY, INFINITY, INFINITY, INFINITY};
+            int8_t Dk[5] = {0, 0, 0, 0, 0};
+            for (int j = 2; j <= 4; ++j)
+                for (int k = 1; k < j; ++k) {
+                    const float c = E(x.child[0], x.box[0], k) + E(x.child[1], x.box[1], j - k);
+                    if (c < D[j]) { D[j] = c; Dk[j] = (int8_t)k; }
+                }
+            const float wide = cn * r.area + D[4];
+            const float leaf = (r.tris <= kAccelLeafMax) ? ct * r.area * (float)r.tris : INFINITY;
+            r.as_leaf = leaf <= wide;
+            const float one = r.as_leaf ? leaf : wide;
+            r.E[0] = INFINITY;
+            r.E[1] = one; r.self[1] = true; r.split[1] = 0;
+            for (int m = 2; m <= 4; ++m) {
+                r.self[m] = one <= D[m];
+                r.E[m] = r.self[m] ? one : D[m];
+                r.split[m] = Dk[m];
+            }
+        }
+    }
+
+    uint32_t first_slot(uint32_t ref) const
+    {
+        while (!(ref & PT_BVH_LEAF_FLAG)) ref = bin.nodes[ref].child[0];
+        return accel_leaf_slot(ref);
+    }
+
+    struct Slot { uint32_t ref; const float* box; bool wide; };
+    void place(uint32_t ref, const float* box, int m, Slot* s, int* n) const
+    {
+        if (ref & PT_BVH_LEAF_FLAG) { s[(*n)++] = {ref, box, false}; return; }
+        const Rec& r = rec[ref];
+        if (r.self[m]) {
+            if (r.as_leaf) s[(*n)++] = {PT_BVH_LEAF_FLAG | ((r.tris - 1u) << 29) | first_slot(ref), box, false};
+            else s[(*n)++] = {ref, box, true};
+            return;
+        }
+        spread(ref, m, s, n);
+    }
+    void spread(uint32_t ref, int m, Slot* s, int* n) const
+    {
+        const AccelNode& x = bin.nodes[ref];
+        const int k = rec[ref].split[m];
+        place(x.child[0], x.box[0], k, s, n);
+        place(x.child[1], x.box[1], m - k, s, n);
+    }
+
+    uint32_t emit(uint32_t b, int depth)
+    {
+        max_depth = std::max(max_depth, depth);
+        Slot s[4];
+        int n = 0;
+        spread(b, 4, s, &n);
+        const uint32_t me = static_cast<uint32_t>(out.nodes.size());
+        out.nodes.emplace_back();
+        uint32_t refs[4];
+        for (int k = 0; k < 4; ++k) refs[k] = (k >= n) ? kAccel4Empty : s[k].wide ? emit(s[k].ref, depth + 1) : s[k].ref;
+        Accel4Node& nd = out.nodes[me];
+        for (int k = 0; k < 4; ++k) {
+            for (int ax = 0; ax < 3; ++ax) {
+                nd.lo[ax][k] = (k < n) ? s[k].box[ax] : 0x1p100f;   // (empty slot: as in Collapser)
+                nd.hi[ax][k] = (k < n) ? s[k].box[3 + ax] : 0x1p100f;
+            }
+            nd.child[k] = refs[k];
+        }
+        return me;
+    }
+};
+
 }  // namespace
 
 int collapse_accel4(const AccelBvh& bin, Accel4* out)
 {
     out->nodes.clear();
     out->nodes.reserve(bin.nodes.size() / 2 + 1);
+    // (PT_COLLAPSE=greedy: the round-1..4 largest-area expansion; the DP measured C3 -0.7% node
+    // visits, +0.5% Msamples/s, profiles/r04_dp)
+    const char* mode = getenv("PT_COLLAPSE");
+    if (!(mode && strcmp(mode, "greedy") == 0)) {
+        const char* cn = getenv("PT_COLLAPSE_CN");
+        const char* ct = getenv("PT_COLLAPSE_CT");
+        DpCollapser dp{bin, *out, cn ? (float)atof(cn) : 1.0f, ct ? (float)atof(ct) : 0.3f};
+        dp.solve();
+        const uint32_t root = dp.emit(0, 0);
+        if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
+        out->depth = dp.max_depth;
+        return PT_OK;
+    }
     Collapser<4, kAccel4LeafTris, Accel4Node, Accel4> col{bin, *out};
     const uint32_t root = col.run(0, 0);
     if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
     out->depth = col.max_depth;
     return PT_OK;
+}
+
+// SAH-style cost of a 4-wide tree (diagnostic): c_node x the surface of every inner node's box
+// as its parent holds it + c_tri x surface x triangles of every leaf child, over the root's.
+double accel4_cost(const Accel4& t, const float* root_box, double cn, double ct)
+{
+    double c = cn * area_of(root_box);
+    for (const Accel4Node& x : t.nodes)
+        for (int k = 0; k < 4; ++k) {
+            if (x.child[k] == kAccel4Empty) continue;
+            const float b[6] = {x.lo[0][k], x.lo[1][k], x.lo[2][k], x.hi[0][k], x.hi[1][k], x.hi[2][k]};
+            c += (x.child[k] & PT_BVH_LEAF_FLAG) ? ct * area_of(b) * accel_leaf_count(x.child[k]) : cn * area_of(b);
+        }
+    return c / area_of(root_box);
 }
 
 }  // namespace pt
@@ -408,8 +548,9 @@ extern "C" int pt_accel_digest(const pt_scene* sc, uint64_t* digest, uint32_t* n
     int rc = pt::build_accel(*sc, &acc);
     if (rc == PT_OK) rc = pt::collapse_accel4(acc, &acc4);
     if (rc != PT_OK) return rc;
-    if (getenv("PT_TIMING")) fprintf(stderr, "pt_accel_digest: SAH cost %.6g, binary depth %d, BVH4 depth %d\n",
-                                     pt::accel_sah_cost(acc), acc.depth, acc4.depth);
+    if (getenv("PT_TIMING"))
+        fprintf(stderr, "pt_accel_digest: SAH cost %.6g, binary depth %d, BVH4 depth %d, BVH4 nodes %zu, BVH4 cost (1, 0.3) %.6g\n",
+                pt::accel_sah_cost(acc), acc.depth, acc4.depth, acc4.nodes.size(), pt::accel4_cost(acc4, acc.root_box, 1.0, 0.3));
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
         const unsigned char* c = static_cast<const unsigned char*>(p);

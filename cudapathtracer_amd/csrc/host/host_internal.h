@@ -114,6 +114,8 @@ struct Accel4 {
     int depth = 0;
 };
 int collapse_accel4(const AccelBvh& bin, Accel4* out);
+// c_node x inner-node surfaces + c_tri x leaf surfaces x triangles, over the root's (diagnostic)
+double accel4_cost(const Accel4& t, const float* root_box, double cn, double ct);
 
 // ---- BVH (BVH.h) ------------------------------------------------------------------------
 int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,
