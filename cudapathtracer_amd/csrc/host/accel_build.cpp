@@ -521,6 +521,51 @@ int collapse_accel4(const AccelBvh& bin, Accel4* out)
     return PT_OK;
 }
 
+// Structural check of a collapsed tree (host diagnostic, pt_accel_digest): every inner node is
+// reached exactly once from the root, every leaf slot of the binary tree exactly once, a node's
+// leaf children hold at most kAccel4LeafTris triangles, and every child box of an inner child
+// contains that child's own child boxes (the nesting the culling relies on).
+int validate_accel4(const AccelBvh& bin, const Accel4& t)
+{
+    const size_t n4 = t.nodes.size(), nslots = bin.leaf_order.size();
+    std::vector<uint8_t> seen_node(n4, 0), seen_slot(nslots, 0);
+    std::vector<uint32_t> todo{0};
+    seen_node[0] = 1;
+    while (!todo.empty()) {
+        const uint32_t i = todo.back();
+        todo.pop_back();
+        const Accel4Node& x = t.nodes[i];
+        uint32_t leaf_tris = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = x.child[k];
+            if (c == kAccel4Empty) continue;
+            if (c & PT_BVH_LEAF_FLAG) {
+                const uint32_t s0 = accel_leaf_slot(c), cnt = accel_leaf_count(c);
+                leaf_tris += cnt;
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    if (s0 + j >= nslots || seen_slot[s0 + j]) return fail(PT_E_SCENE, "validate_accel4: leaf slot %u", s0 + j);
+                    seen_slot[s0 + j] = 1;
+                }
+                continue;
+            }
+            if (c >= n4 || seen_node[c]) return fail(PT_E_SCENE, "validate_accel4: node %u reached twice or out of range", c);
+            seen_node[c] = 1;
+            const Accel4Node& y = t.nodes[c];
+            for (int q = 0; q < 4; ++q) {
+                if (y.child[q] == kAccel4Empty) continue;
+                for (int ax = 0; ax < 3; ++ax)
+                    if (!(y.lo[ax][q] >= x.lo[ax][k] && y.hi[ax][q] <= x.hi[ax][k]))
+                        return fail(PT_E_SCENE, "validate_accel4: node %u child %d leaves its parent's box", c, q);
+            }
+            todo.push_back(c);
+        }
+        if (leaf_tris > kAccel4LeafTris) return fail(PT_E_SCENE, "validate_accel4: node %u has %u leaf triangles", i, leaf_tris);
+    }
+    for (size_t i = 0; i < n4; ++i) if (!seen_node[i]) return fail(PT_E_SCENE, "validate_accel4: node %zu unreachable", i);
+    for (size_t s = 0; s < nslots; ++s) if (!seen_slot[s]) return fail(PT_E_SCENE, "validate_accel4: leaf slot %zu unreachable", s);
+    return PT_OK;
+}
+
 // SAH-style cost of a 4-wide tree (diagnostic): c_node x the surface of every inner node's box
 // as its parent holds it + c_tri x surface x triangles of every leaf child, over the root's.
 double accel4_cost(const Accel4& t, const float* root_box, double cn, double ct)
@@ -547,6 +592,7 @@ extern "C" int pt_accel_digest(const pt_scene* sc, uint64_t* digest, uint32_t* n
     pt::Accel4 acc4;
     int rc = pt::build_accel(*sc, &acc);
     if (rc == PT_OK) rc = pt::collapse_accel4(acc, &acc4);
+    if (rc == PT_OK) rc = pt::validate_accel4(acc, acc4);
     if (rc != PT_OK) return rc;
     if (getenv("PT_TIMING"))
         fprintf(stderr, "pt_accel_digest: SAH cost %.6g, binary depth %d, BVH4 depth %d, BVH4 nodes %zu, BVH4 cost (1, 0.3) %.6g\n",

@@ -116,6 +116,8 @@ struct Accel4 {
 int collapse_accel4(const AccelBvh& bin, Accel4* out);
 // c_node x inner-node surfaces + c_tri x leaf surfaces x triangles, over the root's (diagnostic)
 double accel4_cost(const Accel4& t, const float* root_box, double cn, double ct);
+// every node and leaf slot reached once, <= kAccel4LeafTris leaf triangles per node, nested boxes
+int validate_accel4(const AccelBvh& bin, const Accel4& t);
 
 // ---- BVH (BVH.h) ------------------------------------------------------------------------
 int build_bvh(const std::vector<pt_vec3>& verts, const std::vector<pt_triangle>& tris,

@@ -246,3 +246,32 @@ def test_parallel_host_builds_are_deterministic(tmp_path, monkeypatch):
         out[threads] = (hashlib.sha256(s.arrays()["bvh"].tobytes()).hexdigest(), s.accel_digest())
     assert out["1"] == out["3"] == out["8"]
     assert out["1"][1][1] > 0 and out["1"][1][2] > 0
+
+
+@pytest.mark.parametrize("name", sorted(SCENE_SETS))
+def test_bvh4_collapse_is_a_valid_tree(name, monkeypatch):
+    """The render path's 4-wide tree, from the SAH-optimal DP collapse (default) and from the old
+    greedy one: pt_accel_digest validates it (every inner node and every binary leaf slot reached
+    exactly once, at most 8 leaf triangles per node, child boxes nested in their parent's box) and
+    fails with PT_E_SCENE otherwise.  The DP never needs more nodes than the greedy collapse."""
+    s = load_scene(name, build_bvh=False)
+    if s.view().num_tris < 2:
+        pytest.skip("the render path needs >= 2 triangles")
+    got = {}
+    for mode in ("dp", "greedy"):
+        monkeypatch.setenv("PT_COLLAPSE", mode)
+        got[mode] = s.accel_digest()
+    assert got["dp"][1] <= got["greedy"][1]
+
+
+def test_bvh4_dp_collapse_on_the_standin(tmp_path, monkeypatch):
+    """The same on a reduced stand-in (~24K triangles): valid, and fewer nodes than greedy."""
+    from cudapathtracer_amd import scenes
+    p = scenes.write_sponza_standin(str(tmp_path), scale_tris=0.06)
+    s = pt.Scene()
+    s.load_obj(p, mtl_basepath=os.path.dirname(p) + "/")
+    got = {}
+    for mode in ("dp", "greedy"):
+        monkeypatch.setenv("PT_COLLAPSE", mode)
+        got[mode] = s.accel_digest()
+    assert got["dp"][1] < got["greedy"][1]
