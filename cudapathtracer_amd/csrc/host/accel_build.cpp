@@ -149,8 +149,9 @@ struct Builder {
         if (e - b == 1) return leaf(b, e);
         const size_t mid = split(b, e);
         // a leaf of up to leaf_max triangles when its SAH cost (one test per triangle) is no more
-        // than the split's: node_cost + (n_L A_L + n_R A_R) / A
-        if (e - b <= leaf_max) {
+        // than the split's: node_cost + (n_L A_L + n_R A_R) / A -- never at the root, which must be a
+        // node (a two-triangle scene, e.g. one quad, would otherwise have no node at all)
+        if (e - b <= leaf_max && depth > 0) {
             float lo[3], hi[3], llo[3], lhi[3], rlo[3], rhi[3];
             bounds(b, e, lo, hi);
             bounds(b, mid, llo, lhi);

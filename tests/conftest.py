@@ -18,6 +18,7 @@ SCENE_SETS = {
     "quirks": [("quirks.obj", (0, 0, 0), 1.0, 0)],
     "blob_flip": [("blob.obj", (0.1, -0.2, 0.3), 1.5, 1)],
     "nomtl": [("nomtl.obj", (0, 0, 0), 1.0, 0)],
+    "quad": [("quad.obj", (0, 0, 0), 1.0, 0)],
 }
 
 

@@ -77,6 +77,23 @@ def test_bit_exact_vs_oracle(oracle_mod, cb, integ, flags):
         assert st["node_tests"] > 0 and st["tri_tests"] > 0
 
 
+@pytest.mark.parametrize("integ", [0, 1])
+def test_two_triangle_scene(oracle_mod, integ):
+    """One emissive quad (two triangles): the render path's tree is a root node with two single-
+    triangle leaves -- pt_create used to fail on it (the SAH made the root a leaf)."""
+    s = load_scene("quad")
+    r = pt.Renderer(s, 0)
+    try:
+        w, h, spp = 24, 16, 3
+        img, st = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=3, integrator=integ)
+        ref, cnt = _oracle(oracle_mod, s, w, h, spp, 3, integ)
+        assert _bits_equal(img, ref) == 0
+        assert np.count_nonzero(img) > 0
+        assert st["rays_reference"] == cnt["traces"]
+    finally:
+        r.close()
+
+
 def test_matches_committed_fixture(cb):
     """The committed oracle render (tests/golden) pins both sides across rebuilds."""
     s, r = cb

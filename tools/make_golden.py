@@ -58,10 +58,24 @@ SCENE_SETS = {
     "quirks": [("models/quirks.obj", (0, 0, 0), 1.0, 0)],
     "blob_flip": [("models/blob.obj", (0.1, -0.2, 0.3), 1.5, 1)],
     "nomtl": [("models/nomtl.obj", (0, 0, 0), 1.0, 0)],
+    "quad": [("models/quad.obj", (0, 0, 0), 1.0, 0)],
 }
+
+# two triangles only (one emissive quad facing the camera): the render path's tree is a root node with
+# two single-triangle leaves (accel_build.cpp never makes the root a leaf)
+QUAD_OBJ = ("mtllib quad.mtl\nusemtl panel\nv -1 0 -1\nv 1 0 -1\nv 1 2 -1\nv -1 2 -1\nf 1 2 3\nf 1 3 4\n")
+QUAD_MTL = "newmtl panel\nKd 0.6 0.5 0.4\nKe 3 2.5 2\n"
 
 NOMTL_OBJ = ("v 0 0 0\nv 1 0 0\nv 0 1 0\nv 1 1 0\nusemtl a\nf 1 2 3\n"
              "mtllib does_not_exist.mtl\nf 2 4 3\nusemtl b\nf 1 2 4\n")
+
+
+def write_quad():
+    os.makedirs(os.path.join(SCENES, "models"), exist_ok=True)
+    with open(os.path.join(SCENES, "models", "quad.obj"), "w") as fh:
+        fh.write(QUAD_OBJ)
+    with open(os.path.join(SCENES, "models", "quad.mtl"), "w") as fh:
+        fh.write(QUAD_MTL)
 
 
 def run_ref(args, cwd=None):
@@ -317,6 +331,13 @@ def main():
         with tempfile.TemporaryDirectory() as tmp:
             kat_helpers(tmp, np.random.default_rng(20261017))
         return
+    if sys.argv[1:] == ["--only", "quad"]:
+        write_quad()
+        with tempfile.TemporaryDirectory() as tmp:
+            arrs = ref_scene(tmp, "quad", SCENE_SETS["quad"])
+            np.savez_compressed(os.path.join(GOLD, "scene_quad.npz"), **arrs)
+            print("scene quad", len(arrs["tris"]), "tris, depth", int(arrs["bvh_depth"]))
+        return
     if sys.argv[1:] == ["--only", "ppm"]:
         with tempfile.TemporaryDirectory() as tmp:
             kat_ppm_morton(tmp)
@@ -329,6 +350,7 @@ def main():
     scenes.write_quirks(SCENES)
     with open(os.path.join(SCENES, "models", "nomtl.obj"), "w") as fh:
         fh.write(NOMTL_OBJ)
+    write_quad()
     rng = np.random.default_rng(20261015)
     with tempfile.TemporaryDirectory() as tmp:
         for name, loads in SCENE_SETS.items():
