@@ -39,9 +39,10 @@ out = {
 }
 if "GRBM_GUI_ACTIVE" in c:
     cyc = c["GRBM_GUI_ACTIVE"] / 8.0     # summed over the 8 XCDs
-    b = {"limiter": "a serial chain per walk step -- the node's memory round trip, then the dependent VALU that "
-                    "picks the next address -- and per shading pass (DESIGN.md 6); TD busy counts requests in "
-                    "flight, VALU issue is about half its wave64 rate (0.5 wave64 instructions per SIMD-cycle)",
+    b = {"limiter": "the walk's dependent memory round trips per ray (walk steps): the step's dependent VALU "
+                    "(deferred under the next fetch), its L1 lookups (-18%) and a sixth wave per SIMD each "
+                    "left the rate unchanged, fewer steps moved it (DESIGN.md 6, 10); TD busy counts requests "
+                    "in flight, VALU issue is about half its wave64 rate (0.5 wave64 instructions per SIMD-cycle)",
          "cycles_per_launch": int(cyc)}
     if "SQ_INSTS_VALU" in c:
         # wave64 VALU instructions per SIMD-cycle; the issue ceiling is 0.5 (a wave64 VALU instruction
