@@ -326,8 +326,8 @@ def KERNEL_NAME(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS),
                     help="BASELINE config: scene, image size, spp and bounces (overridable below)")
     ap.add_argument("--width", type=int, default=None)
