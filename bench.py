@@ -209,7 +209,7 @@ def l1_roofline(roof):
     of them runs at ~1 line per CU-cycle however the lines are spread over L2 / Infinity Cache / HBM (10 and
     100 MB tables alike) and however many lanes are masked or out of range.  achieved = the render kernel's
     TCP_TOTAL_CACHE_ACCESSES per CU-cycle from the same profile as `roofline`.  Not the walk's limiter: 18%
-    fewer lookups left the rate unchanged (profiles/r04_topasm); the step's serial chain is."""
+    fewer lookups left the rate unchanged (profiles/r04_topasm); the walk steps per ray are."""
     b = (roof or {}).get("binding") or {}
     x = b.get("l1_lookups_per_cu_cycle")
     if x is None:

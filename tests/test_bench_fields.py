@@ -1,0 +1,75 @@
+"""bench.py's roofline blocks on CPU: every field means what its block says.
+
+The HBM `roofline` takes its measured traffic only from the profiles/traffic.json entry of this exact
+kernel source hash and config; the algorithmic bytes live in `cache_roofline` (L2 roof) and the L1
+lookup rate in `l1_roofline`, marked as not the binding resource.  No field exceeds its own peak.
+"""
+import json
+import os
+import types
+
+import bench
+
+
+COUNTS = dict(node_tests=6_621_908_388, lds_node_tests=0, tri_tests=1_917_249_061, walk_lane_slots=10_493_000_000,
+              leaf_steps=1_917_249_061, accel_fallbacks=195, spill_entries=0, walk_cycles=758, shade_cycles=242,
+              shade_lane_slots=646_000_000, samples=1920 * 1080 * 256, rays_traced=507_000_000)
+
+
+def _args(tmp_json, **kw):
+    a = dict(flags=0, integrator=0, spp=256, bounces=3, sim_shards=1, traffic_json=tmp_json)
+    a.update(kw)
+    return types.SimpleNamespace(**a)
+
+
+def test_traffic_entry_matches_hash_and_config(tmp_path):
+    sha = bench.kernel_source_sha256()
+    p = tmp_path / "t.json"
+    e = {"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha, "traffic_bytes_per_launch": 4e11,
+         "kernel_ms": 91.0, "profile": "profiles/x", "binding": {"l1_lookups_per_cu_cycle": 0.8}}
+    p.write_text(json.dumps({"entries": [e, dict(e, config=[1024, 1024, 64, 8, 0, 1], traffic_bytes_per_launch=3e10)]}))
+    assert bench.traffic_entry(str(p), [1920, 1080, 256, 3, 0, 1], sha)["traffic_bytes_per_launch"] == 4e11
+    assert bench.traffic_entry(str(p), [1920, 1080, 256, 3, 0, 2], sha) is None      # another shard count
+    assert bench.traffic_entry(str(p), [1920, 1080, 256, 3, 0, 1], "0" * 64) is None  # another kernel
+    assert bench.traffic_entry(str(tmp_path / "missing.json"), [1], sha) is None
+
+
+def test_roofline_fields_stay_below_their_peaks(tmp_path):
+    sha = bench.kernel_source_sha256()
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"entries": [{"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha,
+                                          "traffic_bytes_per_launch": 397_000_000_000, "kernel_ms": 91.6,
+                                          "profile": "profiles/x", "binding": {"l1_lookups_per_cu_cycle": 0.803}}]}))
+    kms = 90.3
+    roof = bench.roofline(COUNTS, kms, 1920, 1080, _args(str(p)), 1)
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s"
+    assert abs(roof["achieved"] - 397e9 / (kms * 1e-3) / 1e9) < 0.01
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-4
+    assert roof["achieved"] <= roof["peak"]
+    assert not any(k.startswith("algorithmic") for k in roof)   # algorithmic bytes are not HBM bytes
+    l1 = bench.l1_roofline(roof)
+    assert l1["binding"] is False and l1["achieved"] <= l1["peak"] and l1["frac"] == 0.803
+    cache = bench.cache_roofline(dict(COUNTS, spp=256), kms)
+    assert cache["bound"] == "l2" and cache["achieved"] <= cache["peak"]
+    alg = (COUNTS["node_tests"] * bench.NODE_BYTES + COUNTS["tri_tests"] * bench.TRI_BYTES
+           + COUNTS["rays_traced"] * 64 + 1920 * 1080 * 12)
+    assert abs(cache["algorithmic_bytes_per_launch"] - alg) <= 1
+
+
+def test_roofline_is_null_without_a_matching_profile(tmp_path):
+    roof = bench.roofline(COUNTS, 90.0, 1920, 1080, _args(str(tmp_path / "none.json")), 1)
+    assert roof["frac"] is None and roof["traffic"] is None and roof["achieved"] is None
+    assert bench.l1_roofline(roof) is None
+
+
+def test_committed_traffic_json_covers_the_bench_configs():
+    """profiles/traffic.json holds entries of the committed kernel for the default bench line (C3),
+    the other BASELINE configs and the shard launches of N = 2, 4, 8."""
+    path = os.path.join(bench.ROOT, "profiles", "traffic.json")
+    sha = bench.kernel_source_sha256()
+    for cfg in ([1920, 1080, 256, 3, 0, 1], [1024, 1024, 64, 8, 0, 1], [1920, 1080, 1024, 3, 0, 1],
+                [3840, 2160, 4096, 16, 0, 1], [1920, 1080, 256, 3, 1, 1], [1920, 1080, 256, 3, 0, 2],
+                [1920, 1080, 256, 3, 0, 4], [1920, 1080, 256, 3, 0, 8]):
+        e = bench.traffic_entry(path, cfg, sha)
+        assert e is not None, cfg
+        assert e["traffic_bytes_per_launch"] / (e["kernel_ms"] * 1e-3) / 1e9 <= bench.HBM_PEAK_GBS
