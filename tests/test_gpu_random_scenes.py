@@ -127,16 +127,27 @@ def test_trace_matches_the_reference_walk(soup):
     assert np.count_nonzero(rt >= 0) > n // 10   # the soup is hit
 
 
+@pytest.mark.parametrize("flags", [0, pt.PT_FLAG_REFERENCE_TRAVERSAL, pt.PT_FLAG_REFERENCE_BVH])
 @pytest.mark.parametrize("integ", [0, 1])
-def test_render_matches_the_oracle(soup, integ):
+def test_render_matches_the_oracle(soup, integ, flags):
+    """The wavefront kernel (flags 0), the tile kernel in the reference's traversal order and the
+    reference-BVH walk, each against the oracle; the default path also as three tile shards summed."""
     import oracle
     seed, s, r = soup
     w, h, spp = 32, 24, 4
-    img, st = r.render(pt.make_camera(width=w, height=h, **CAM), w, h, spp, bounces=3, integrator=integ)
+    cam = pt.make_camera(width=w, height=h, **CAM)
+    img, st = r.render(cam, w, h, spp, bounces=3, integrator=integ, flags=flags)
     osc = oracle.OracleScene(s.arrays())
     ocam = oracle.camera(CAM["pos"], CAM["dist_from_film"], CAM["focal_length"], CAM["radius"], w, h)
     ref, cnt = oracle.render(osc, ocam, w, h, spp, 3, integ, 1234)
-    diff = int(np.count_nonzero(img.view(np.uint32) != ref.astype(np.float32).view(np.uint32)))
+    ref32 = ref.astype(np.float32).view(np.uint32)
+    diff = int(np.count_nonzero(img.view(np.uint32) != ref32))
     assert diff == 0, diff
     assert st["rays_reference"] == cnt["traces"]
     assert np.count_nonzero(img) > 0
+    if flags == 0:
+        acc = np.zeros_like(img)
+        for k in range(3):
+            part, _ = r.render(cam, w, h, spp, bounces=3, integrator=integ, shard_index=k, shard_count=3)
+            acc += part
+        assert int(np.count_nonzero(acc.view(np.uint32) != ref32)) == 0
