@@ -38,6 +38,11 @@ for v in sorted(os.listdir(src)):
         out["ta_busy"] = agg.get("TA_TA_BUSY_sum", 0) / 256 / cyc
         out["valu_per_simd_cycle"] = agg.get("SQ_INSTS_VALU", 0) / 1024 / cyc
         out["l1_lookups_per_cu_cycle"] = agg.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0) / 256 / cyc
+        out["ta_stalled_by_tc"] = agg.get("TA_ADDR_STALLED_BY_TC_CYCLES_sum", 0) / 256 / cyc
+    hits, misses = agg.get("TCC_HIT_sum", 0.0), agg.get("TCC_MISS_sum", 0.0)
+    if hits + misses:
+        out["l2_hit_rate"] = hits / (hits + misses)
+        out["l2_requests_G"] = (hits + misses) / 1e9
     out["l1_lookups_G"] = agg.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0) / 1e9
     out["valu_G"] = agg.get("SQ_INSTS_VALU", 0) / 1e9
     out["fetch_GB_x2"] = agg.get("FETCH_SIZE", 0) * 1024 * 2 / 1e9
