@@ -73,9 +73,10 @@ struct Args {
     const DNode4* nodes4;           // render-path BVH4 (collapsed SAH BVH)
     const DTri* acc_tris;           // its leaf-order triangle records (id, reference rank, parent)
     const uint32_t* rparent;        // reference BVH: parent of each node (winner chain check)
-    const RNode* wbox;              // per render-path slot: its triangle's reference parent node (left/right
-                                    // replaced by the parent's index) -- the winner check's box, fetched
-                                    // with the slot's ids
+    const float4* hrec;             // per render-path slot, 48 B: {reference parent's lo, hi.x}, {hi.y, hi.z,
+                                    // parent index, triangle id}, {normal, material} -- the winner check's
+                                    // words (both integrators) and, for integrator 0, the checked hit's
+                                    // shading normal and material on the same line
     uint32_t* spill;                // LDS-stack overflow, entry k of lane g at spill[(k-kRing)*stride + g]
     uint32_t spill_stride;
     uint32_t cold_stride;           // records of the cold array (one per resident lane)
@@ -971,14 +972,19 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
     // the words every pass needs: four 16-B cells (issued first: their round trip overlaps the
     // winner check's two dependent ones)
     const uint4 k0 = R.ld4(CW_N), k1 = R.ld4(CW_RNG_V0), k2 = R.ld4(CW_WGT), k3 = R.ld4(CW_WGT + 4);
+    // the checked winner's slot: the bounce that follows reads its normal and material from the slot's
+    // record (the line the check just fetched) instead of the triangle's shading record
+    uint32_t hslot = kNone;
     if (state == ST_CHECK) {
         SEC(SEC_CHECK);
         // the winner must be a triangle the reference tests (DESIGN.md "Traversal"); if not
         // (rare), the exact reference-BVH walk redoes the ray
-        const float4 C = a.acc_tris[htri].c;
-        const float4 b0 = reinterpret_cast<const float4*>(a.wbox + htri)[0], b1 = reinterpret_cast<const float4*>(a.wbox + htri)[1];
-        htri = (int32_t)__float_as_uint(C.y);
+        const uint32_t slot = (uint32_t)htri;
+        const float4* hr = a.hrec + 3 * (size_t)slot;
+        const float4 b0 = hr[0], b1 = hr[1];
+        htri = (int32_t)__float_as_uint(b1.w);
         state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
+        if (state == ST_SHADE && a.num_spheres == 0) hslot = slot;
     }
     int n = (int)k0.x, i = (int)k0.y;
     uint32_t fl = k0.z;
@@ -1097,7 +1103,14 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
             const V3 pos = ro + rd * t;
             V3 normal;
             C3 m_em, m_alb;   // the material's emission and albedo (materialDesc, f64)
-            if (a.shade_m && (uint32_t)tri < a.num_tris) {
+            if (hslot != kNone) {   // (a checked hit: finite t, so tri is the winner)
+                const float4 q2 = a.hrec[3 * (size_t)hslot + 2];
+                const DMat* cm = a.mats + (int32_t)__float_as_uint(q2.w);
+                normal = v3(q2.x, q2.y, q2.z);
+                m_em = mat_emission(cm);
+                m_alb = mat_albedo(cm);
+                hslot = kNone;
+            } else if (a.shade_m && (uint32_t)tri < a.num_tris) {
                 const float4* rec = a.shade_m + 3 * (size_t)(uint32_t)tri;
                 const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
                 normal = v3(q0.x, q0.y, q0.z);
@@ -1605,9 +1618,9 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
     const uint4 k0 = R.ld4(HW_N);
     if (state == ST_CHECK) {
         SEC(SEC_CHECK);
-        const float4 C = a.acc_tris[htri].c;
-        const float4 b0 = reinterpret_cast<const float4*>(a.wbox + htri)[0], b1 = reinterpret_cast<const float4*>(a.wbox + htri)[1];
-        htri = (int32_t)__float_as_uint(C.y);
+        const float4* hr = a.hrec + 3 * (size_t)(uint32_t)htri;
+        const float4 b0 = hr[0], b1 = hr[1];
+        htri = (int32_t)__float_as_uint(b1.w);
         state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
     }
     int n = (int)k0.x;
@@ -2460,7 +2473,7 @@ struct pt_ctx {
     DNode4* nodes4 = nullptr;
     DTri* acc_tris = nullptr;
     uint32_t* rparent = nullptr;
-    RNode* wbox = nullptr;
+    float4* hrec = nullptr;
     float* tone_thr = nullptr;        // output step: the host libm's 255 code boundaries (+ t[0] = 0)
     bool tone_ok = false;
     float4* spheres = nullptr;        // sphere primitives (center, radius)
@@ -2799,7 +2812,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (!(sc->bvh[i].left & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].left] = i;
         if (!(sc->bvh[i].right & PT_BVH_LEAF_FLAG)) rpar[sc->bvh[i].right] = i;
     }
-    // per render-path slot: the reference parent's node of its triangle (Args::wbox)
+    // per render-path slot: the reference parent's node of its triangle (into Args::hrec below)
     std::vector<RNode> wb(std::max<size_t>(at.size(), 1));
     for (size_t sl = 0; sl < at.size(); ++sl) {
         uint32_t parent;
@@ -2807,6 +2820,21 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         wb[sl] = rn[parent];
         wb[sl].left = parent;
         wb[sl].right = 0u;
+    }
+    // per render-path slot: the winner check's box, parent and triangle id, and the shading normal and
+    // material (Args::hrec)
+    std::vector<float4> hr((size_t)3 * std::max<size_t>(at.size(), 1));
+    for (size_t sl = 0; sl < at.size(); ++sl) {
+        uint32_t tid;
+        memcpy(&tid, &at[sl].c.y, 4);
+        const RNode& b = wb[sl];
+        float fpar, ftid, fmat;
+        memcpy(&fpar, &b.left, 4);
+        memcpy(&ftid, &tid, 4);
+        memcpy(&fmat, &sc->tris[tid].mat, 4);
+        hr[3 * sl] = make_float4(b.lo[0], b.lo[1], b.lo[2], b.hi[0]);
+        hr[3 * sl + 1] = make_float4(b.hi[1], b.hi[2], fpar, ftid);
+        hr[3 * sl + 2] = make_float4(sc->tris[tid].norm.x, sc->tris[tid].norm.y, sc->tris[tid].norm.z, fmat);
     }
     // last-bounce light probe (shade_lane begin_trace): every triangle whose material has
     // emission.r != 0 (the integrator's emission test, kernel.cu:453 -- not the caller's light list)
@@ -2912,7 +2940,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
     if ((rc = upload(&c->nodes, dn)) || (rc = upload(&c->rnodes, rn)) || (rc = upload(&c->tris_leaf, tl)) ||
         (rc = upload(&c->tris_orig, to)) || (rc = upload(&c->shade, sh)) || (!shm.empty() && (rc = upload(&c->shade_m, shm))) || (rc = upload(&c->mats, mt)) ||
         (rc = upload(&c->lights, lt)) || (rc = upload(&c->jump, jump)) || (rc = upload(&c->tone_thr, tone)) || (rc = upload(&c->spheres, sp)) ||
-        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) || (rc = upload(&c->wbox, wb)) ||
+        (rc = upload(&c->nodes4, an)) || (rc = upload(&c->acc_tris, at)) || (rc = upload(&c->rparent, rpar)) || (rc = upload(&c->hrec, hr)) ||
         (rc = upload(&c->tri_counts, std::vector<uint32_t>(std::max<uint32_t>(nt, 1u), 0u))) ||
         (rc = upload(&c->emis, em))) {
         pt_destroy(c);
@@ -2933,7 +2961,7 @@ void pt_destroy(pt_ctx* c)
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->nodes, c->rnodes, c->tris_leaf, c->tris_orig, c->shade, c->mats,
                     c->lights, c->jump, c->jump_bytes, c->shade_m, c->scratch_out,
-                    c->nodes4, c->acc_tris, c->rparent, c->wbox,
+                    c->nodes4, c->acc_tris, c->rparent, c->hrec,
                     c->tone_thr, c->spheres, c->tri_counts, c->emis};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -3067,7 +3095,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
     a.nodes4 = c->nodes4;
     a.acc_tris = c->acc_tris;
     a.rparent = c->rparent;
-    a.wbox = c->wbox;
+    a.hrec = c->hrec;
     memcpy(a.acc_root, c->acc_root, sizeof(a.acc_root));
     // the render-path BVH's box margin assumes ray origins within ~2^6 of the scene extent
     const float cam_ext = std::fmax(std::fabs(cam->pos.x), std::fmax(std::fabs(cam->pos.y), std::fabs(cam->pos.z)));
