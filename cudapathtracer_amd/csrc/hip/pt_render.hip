@@ -107,6 +107,9 @@ struct Args {
                                     // dependent ones (shade, then mats); null: shade + mats
     const DTri* emis;               // last-bounce light probe: the emissive triangles' records (see begin_trace)
     uint32_t num_emis;              // 0 = probe off
+    uint32_t rec_shading;           // integrator 0's checked hits take their normal and material from hrec (a
+                                    // scene larger than the LDS top); 0: from shade_m by triangle id (a tree
+                                    // held whole in LDS -- C2 -- where that one fetch is an L2 hit anyway)
     unsigned long long* lane_times; // diagnostic (PT_LANE_TIMING): wall clock of each lane's end, then each
                                     // wave's start and exit (render_unidir_wf), or null
     uint32_t head;                  // integrator 1 on the wavefront kernel (init_pixel_states' replay)
@@ -984,7 +987,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
         const float4 b0 = hr[0], b1 = hr[1];
         htri = (int32_t)__float_as_uint(b1.w);
         state = ref_tested_box(b0, b1, __float_as_uint(b1.z), ro, rd, a.rnodes, a.rparent) ? ST_SHADE : ST_SLOW;
-        if (state == ST_SHADE && a.num_spheres == 0) hslot = slot;
+        if (state == ST_SHADE && a.num_spheres == 0 && a.rec_shading) hslot = slot;
     }
     int n = (int)k0.x, i = (int)k0.y;
     uint32_t fl = k0.z;
@@ -3149,6 +3152,8 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         // the whole tree staged in LDS (small scenes: C2): integrator 0's walk steps read it there too
         // (PT_WF_LDS_TREE=0: memory loads, as for a tree larger than the top)
         const bool lds_tree = c->wf_lds_tree && c->n4 > 0 && b.top_nodes >= c->n4;
+        // (C2: 7181 with the record's second fetch against 7267 by triangle id; C3 the other way)
+        b.rec_shading = lds_tree ? 0u : 1u;
         uint32_t blocks = (uint32_t)c->num_cus * (wpc / 4 ? wpc / 4 : 1);
         // Work units: a pixel's samples run in sequence, so a unit lasts one pixel's time and the
         // kernel's end waits for the last units started.  Whole pixels first; the last `ntail`
