@@ -317,6 +317,24 @@ def make_reduce(dist, backend, rank):
     return gloo_reduce
 
 
+class stdout_to_stderr:
+    """Route file descriptor 1 to stderr for the block: the process-group setup's own banners (RCCL's
+    version lines, gloo's peer messages) are printed by C++ to stdout, which must carry rank 0's one
+    JSON line only."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def KERNEL_NAME(args):
     if args.flags & 1:   # PT_FLAG_REFERENCE_TRAVERSAL: the tile kernel
         return "render_tiles"
@@ -375,10 +393,12 @@ def main():
         local = local % ndev
     torch.cuda.set_device(local)
     if distributed:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        with stdout_to_stderr():   # (communicator setup, and a first collective: no banner on stdout)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+            dist.barrier()
 
     os.makedirs(args.cache_dir, exist_ok=True)
     kind = CONFIGS[args.config]["scene"]
