@@ -23,6 +23,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with:
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -322,14 +323,21 @@ class stdout_to_stderr:
     version lines, gloo's peer messages) are printed by C++ to stdout, which must carry rank 0's one
     JSON line only."""
 
-    def __enter__(self):
+    @staticmethod
+    def _flush_all():
+        # Python's buffer, then C stdio's (RCCL / gloo print through libc; a pipe makes stdout fully
+        # buffered, so text left there would be flushed after rank 0's JSON line at exit)
         sys.stdout.flush()
+        ctypes.CDLL(None).fflush(None)
+
+    def __enter__(self):
+        self._flush_all()
         self.saved = os.dup(1)
         os.dup2(2, 1)
         return self
 
     def __exit__(self, *exc):
-        sys.stdout.flush()
+        self._flush_all()
         os.dup2(self.saved, 1)
         os.close(self.saved)
         return False

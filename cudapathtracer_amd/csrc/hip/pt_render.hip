@@ -2717,6 +2717,10 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
         if (timing && rc4 == PT_OK) fprintf(stderr, "pt_create: render BVH SAH cost %.6g\n", pt::accel_sah_cost(acc));
         if (rc4 == PT_OK) rc4 = pt::collapse_accel4(acc, &acc4);
         lap("BVH4 collapse");
+        // the structural check (every node and slot reached once, <= 8 leaf triangles per node, nested
+        // boxes) is O(nodes): the walk's exactness argument and its 8-bit leaf masks rely on it
+        if (rc4 == PT_OK) rc4 = pt::validate_accel4(acc, acc4);
+        lap("BVH4 validate");
         if (rc4 != PT_OK) { delete c; return bail(rc4); }
         // Node order: the kTopNodesMax nodes most likely to be visited first (best-first by box
         // surface area from the root: a connected top subtree, staged in LDS by the wavefront

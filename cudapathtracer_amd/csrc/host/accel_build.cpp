@@ -455,8 +455,12 @@ struct DpCollapser {
     }
 
     struct Slot { uint32_t ref; const float* box; bool wide; };
+    mutable bool overflow = false;   // place() was asked for a fifth slot (a malformed DP table)
     void place(uint32_t ref, const float* box, int m, Slot* s, int* n) const
     {
+        // a slot budget m < 1 or a fifth slot cannot come from a well-formed table (split[] in 1..m-1);
+        // refuse it instead of writing past the node's 4 slots
+        if (m < 1 || *n >= 4) { overflow = true; return; }
         if (ref & PT_BVH_LEAF_FLAG) { s[(*n)++] = {ref, box, false}; return; }
         const Rec& r = rec[ref];
         if (r.self[m]) {
@@ -506,11 +510,22 @@ int collapse_accel4(const AccelBvh& bin, Accel4* out)
     // visits, +0.5% Msamples/s, profiles/r04_dp)
     const char* mode = getenv("PT_COLLAPSE");
     if (!(mode && strcmp(mode, "greedy") == 0)) {
-        const char* cn = getenv("PT_COLLAPSE_CN");
-        const char* ct = getenv("PT_COLLAPSE_CT");
-        DpCollapser dp{bin, *out, cn ? (float)atof(cn) : 1.0f, ct ? (float)atof(ct) : 0.3f};
+        // cost knobs: finite and positive, else every comparison of the DP fails and no slot split is
+        // ever chosen (PT_E_INVALID names the knob instead of building a malformed tree)
+        float knob[2] = {1.0f, 0.3f};
+        const char* names[2] = {"PT_COLLAPSE_CN", "PT_COLLAPSE_CT"};
+        for (int i = 0; i < 2; ++i)
+            if (const char* v = getenv(names[i])) {
+                char* end = nullptr;
+                const double x = strtod(v, &end);
+                if (end == v || *end != '\0' || !std::isfinite(x) || !(x > 0.0) || x > 1e30)
+                    return fail(PT_E_INVALID, "collapse_accel4: %s=\"%s\" is not a finite positive number", names[i], v);
+                knob[i] = (float)x;
+            }
+        DpCollapser dp{bin, *out, knob[0], knob[1]};
         dp.solve();
         const uint32_t root = dp.emit(0, 0);
+        if (dp.overflow) return fail(PT_E_SCENE, "collapse_accel4: a node was given more than 4 slots");
         if (root != 0) return fail(PT_E_SCENE, "collapse_accel4: internal error");
         out->depth = dp.max_depth;
         return PT_OK;

@@ -84,3 +84,77 @@ def test_gloo_two_rank_render_equals_single(tmp_path):
     osc = oracle.OracleScene(s.arrays())
     full, _ = oracle.render(osc, oracle.camera((0.0, 1.0, 3.0), 1.0, 3.0, 0.0, w, h), w, h, spp, 3, 0, 1234)
     assert assembled.tobytes() == full.astype(np.float32).tobytes()
+
+
+def _gpu_worker(rank, world, port, objpath, w, h, spp, outdir):
+    """One rank of the GPU multi-process test: libptamd renders this rank's tile shard on GPU 0 (both
+    integrators; integrator 0 through the host-buffer entry point, integrator 1 into a torch device
+    tensor as bench.py does), gloo sums the shards on rank 0, which also renders the whole frame."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import cudapathtracer_amd as pt
+    from cudapathtracer_amd import scenes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = pt.Scene()
+    s.load_obj(objpath, mtl_basepath=os.path.dirname(objpath) + "/")
+    s.build_bvh()
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    with pt.Renderer(s, 0) as r:
+        for integ in (pt.PT_INTEGRATOR_UNIDIR, pt.PT_INTEGRATOR_HEAD):
+            if integ == pt.PT_INTEGRATOR_UNIDIR:
+                img, st = r.render(cam, w, h, spp, bounces=3, integrator=integ, seed=1234,
+                                   shard_index=rank, shard_count=world)
+                fb = torch.from_numpy(img.copy())
+            else:
+                d = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda:0")
+                st = r.render_device(cam, d.data_ptr(), w, h, spp, bounces=3, integrator=integ, seed=1234,
+                                     shard_index=rank, shard_count=world,
+                                     stream_ptr=torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                fb = d.cpu()
+            np.save(os.path.join(outdir, "shard_%d_r%d.npy" % (integ, rank)), fb.numpy())
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+            n = torch.tensor([st["samples"]], dtype=torch.int64)
+            dist.all_reduce(n)
+            if rank == 0:
+                full, _ = r.render(cam, w, h, spp, bounces=3, integrator=integ, seed=1234)
+                np.save(os.path.join(outdir, "assembled_%d.npy" % integ), fb.numpy())
+                np.save(os.path.join(outdir, "full_%d.npy" % integ), full)
+                np.save(os.path.join(outdir, "samples_%d.npy" % integ), n.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_two_rank_libptamd_shards_reduce_to_full_frame(tmp_path):
+    """SURVEY 8e on the GPU, across processes: two freshly spawned rank processes
+    (the spawn start method: each a new interpreter; this file runs before any in-process GPU test)
+    render their interleaved 8x8-tile shards of a 320x180 stand-in frame with libptamd on GPU 0, and a
+    gloo reduce(SUM) assembles rank 0's image.  It must equal libptamd's single-process render of the
+    whole frame bit for bit, for both integrators; each shard is zero outside its own tiles and the
+    sample counts add up to W*H*spp.  (RCCL refuses two ranks on one device, so the reduce is gloo's;
+    bench.py's RCCL leg differs only in the transport.)"""
+    from cudapathtracer_amd import scenes
+    d = tmp_path / "scene"
+    d.mkdir()
+    objpath = scenes.write_sponza_standin(str(d))
+    w, h, spp, world = 320, 180, 16, 2
+    mp.start_processes(_gpu_worker, args=(world, _free_port(), objpath, w, h, spp, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    for integ in (0, 1):
+        assembled = np.load(str(tmp_path / ("assembled_%d.npy" % integ)))
+        full = np.load(str(tmp_path / ("full_%d.npy" % integ)))
+        assert assembled.shape == full.shape == (h, w, 3)
+        assert int(np.load(str(tmp_path / ("samples_%d.npy" % integ)))[0]) == w * h * spp
+        assert np.count_nonzero(full) > 0
+        assert assembled.view(np.uint32).tobytes() == full.view(np.uint32).tobytes(), integ
+        for k in range(world):
+            sh = np.load(str(tmp_path / ("shard_%d_r%d.npy" % (integ, k)))).reshape(-1, 3)
+            mine = np.zeros(w * h, dtype=bool)
+            mine[shard.shard_pixels(w, h, k, world)] = True
+            assert not np.any(sh[~mine]), (integ, k)
+            assert sh[mine].view(np.uint32).tobytes() == full.reshape(-1, 3)[mine].view(np.uint32).tobytes()

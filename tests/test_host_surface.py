@@ -275,3 +275,20 @@ def test_bvh4_dp_collapse_on_the_standin(tmp_path, monkeypatch):
         monkeypatch.setenv("PT_COLLAPSE", mode)
         got[mode] = s.accel_digest()
     assert got["dp"][1] < got["greedy"][1]
+
+
+@pytest.mark.parametrize("knob", ["PT_COLLAPSE_CN", "PT_COLLAPSE_CT"])
+@pytest.mark.parametrize("value", ["nan", "inf", "-1", "0", "abc", ""])
+def test_bvh4_collapse_rejects_bad_cost_knobs(knob, value, monkeypatch):
+    """The DP collapse's cost knobs must be finite and positive: with NaN/inf costs every comparison of
+    the DP fails, no slot split is chosen and the emitted node could overflow its 4 slots.  A bad
+    value is refused with PT_E_INVALID (naming the knob) instead of building a malformed tree; a good
+    one still builds (accel_build.cpp)."""
+    s = load_scene("cornell", build_bvh=False)
+    monkeypatch.delenv("PT_COLLAPSE", raising=False)
+    monkeypatch.setenv(knob, value)
+    with pytest.raises(pt.PtError) as ei:
+        s.accel_digest()
+    assert knob in str(ei.value)
+    monkeypatch.setenv(knob, "0.5")
+    assert s.accel_digest()[1] > 0

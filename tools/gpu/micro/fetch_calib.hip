@@ -82,6 +82,35 @@ __global__ __launch_bounds__(256) void cells(uint4* __restrict__ buf, uint32_t n
     for (int c = 0; c < 4; ++c) buf[(size_t)c * n + g] = make_uint4(v[c].y + 1u, v[c].z, v[c].w, v[c].x);
 }
 
+// The DRAM-request calibration (round 5): the same gather and cell shapes on tables that stay resident
+// in a cache, so that TCC_EA0_RDREQ_DRAM / TCC_EA0_WRREQ_DRAM can be compared with TCC_EA0_RDREQ / WRREQ:
+// a counter that excludes Infinity-Cache hits reads ~0 on the 32 MB table's measured launch (every line
+// was brought in by the warm launch just before it); one that counts them reads like RDREQ.
+template <int kTag>
+__global__ __launch_bounds__(256) void gather7_res(const uint4* __restrict__ buf, uint32_t mask, uint32_t* out)
+{
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    const char* base = reinterpret_cast<const char*>(buf) + (size_t)perm(g, mask) * 128;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const uint4 v = *reinterpret_cast<const uint4*>(base + 16 * k);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    out[g] = acc;
+}
+template <int kTag>
+__global__ __launch_bounds__(256) void cells_res(uint4* __restrict__ buf, uint32_t n)
+{
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    uint4 v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = buf[(size_t)c * n + g];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) buf[(size_t)c * n + g] = make_uint4(v[c].y + 1u, v[c].z, v[c].w, v[c].x);
+}
+
 int main()
 {
     // 8 GiB of 128-B lines (>> 256 MiB Infinity Cache); 2^26 lines
@@ -116,6 +145,26 @@ int main()
     CK(hipDeviceSynchronize());
     printf("cells known_read_bytes %llu known_write_bytes %llu\n", (unsigned long long)ncell * 64,
            (unsigned long long)ncell * 64);
+    // resident tables: warm launch (tag 0), then the measured launch (tag 1) on the same lines
+    // 32 MB table = 2^18 lines (Infinity-Cache resident, 8x an XCD's L2); 4M lanes: each line 16 times
+    hipLaunchKernelGGL(stream, dim3(8192), dim3(256), 0, 0, buf, bytes / 16, out);   // (flush)
+    hipLaunchKernelGGL((gather7_res<0>), dim3(lanes / 256), dim3(256), 0, 0, buf, (1u << 18) - 1, out);
+    hipLaunchKernelGGL((gather7_res<1>), dim3(lanes / 256), dim3(256), 0, 0, buf, (1u << 18) - 1, out);
+    CK(hipDeviceSynchronize());
+    printf("gather7_res<1> table 32 MiB (resident in the Infinity Cache after gather7_res<0>), %u lane-lines of 112 B "
+           "(%llu B requested by lanes), distinct lines 2^18\n", lanes, (unsigned long long)lanes * 112);
+    // 2 MB table = 2^14 lines: resident in every XCD's 4 MiB L2
+    hipLaunchKernelGGL((gather7_res<2>), dim3(lanes / 256), dim3(256), 0, 0, buf, (1u << 14) - 1, out);
+    hipLaunchKernelGGL((gather7_res<3>), dim3(lanes / 256), dim3(256), 0, 0, buf, (1u << 14) - 1, out);
+    CK(hipDeviceSynchronize());
+    printf("gather7_res<3> table 2 MiB (L2 resident after gather7_res<2>), %u lane-lines\n", lanes);
+    // 32 MB of cells (2^19 lanes x 4 x 16 B) read and written twice: warm <0>, measured <1>
+    const uint32_t ncr = 1u << 19;
+    hipLaunchKernelGGL((cells_res<0>), dim3(ncr / 256), dim3(256), 0, 0, buf, ncr);
+    hipLaunchKernelGGL((cells_res<1>), dim3(ncr / 256), dim3(256), 0, 0, buf, ncr);
+    CK(hipDeviceSynchronize());
+    printf("cells_res<1> 32 MiB read + 32 MiB written (resident after cells_res<0>) known_read_bytes %llu known_write_bytes %llu\n",
+           (unsigned long long)ncr * 64, (unsigned long long)ncr * 64);
     CK(hipFree(buf));
     CK(hipFree(out));
     return 0;
