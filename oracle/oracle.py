@@ -56,7 +56,7 @@ class OCounters(C.Structure):
 
 _libs = {}
 # sensitivity variants of the restatement (oracle/Makefile VARIANTS; tools/parity/ref_gap.py)
-VARIANTS = ("fma", "fma_notri", "libm", "ulp1", "ulp2", "unfused", "nvcc")
+VARIANTS = ("fma", "fma_notri", "libm", "ulp1", "ulp2", "unfused", "nvcc", "fma_tri", "fmal_tri", "fmar_tri")
 
 
 def lib(variant=None):

@@ -249,27 +249,60 @@ void or_sincos(float theta, float* s_out, float* c_out)
 
 /* -------------------------------------------------------------- geometry */
 /* modelLoader.h:49-83 triIntersect.  (OR_TRI_NO_CONTRACT: the fma_notri sensitivity variant keeps this one
- * function uncontracted while the rest of the build contracts, tools/parity/ref_gap.py) */
+ * function uncontracted while the rest of the build contracts; OR_TRI_CONTRACT: the fma_tri variant
+ * contracts this one function only, as the compiler chooses; OR_TRI_FMA = 1 / 2: the fmal_tri / fmar_tri
+ * variants spell the contraction out -- vec3.h's a*b + c*d and a*b - c*d with the LEFT product fused
+ * (fma(a, b, c*d), fma(a, b, -(c*d)): LLVM's DAG combiner folds (fadd (fmul a b) z) first, GCC's
+ * widening_mul converts the first product in statement order) or the RIGHT one (fma(c, d, a*b),
+ * fma(-c, d, a*b)); the dot product's last term fuses either way.  tools/parity/ref_gap.py) */
+#if defined(OR_TRI_FMA)
+static inline float tdot(or_vec3 a, or_vec3 b)
+{
+#if OR_TRI_FMA == 1
+    return fmaf(a.z, b.z, fmaf(a.x, b.x, a.y * b.y));
+#else
+    return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x));
+#endif
+}
+static inline float tdiff(float a, float b, float c, float d)   /* a*b - c*d */
+{
+#if OR_TRI_FMA == 1
+    return fmaf(a, b, -(c * d));
+#else
+    return fmaf(-c, d, a * b);
+#endif
+}
+static inline or_vec3 tcross(or_vec3 a, or_vec3 b)
+{
+    return v3(tdiff(a.y, b.z, a.z, b.y), tdiff(a.z, b.x, a.x, b.z), tdiff(a.x, b.y, a.y, b.x));
+}
+#else
+#define tdot vdot
+#define tcross vcross
+#endif
 #ifdef OR_TRI_NO_CONTRACT
 __attribute__((optimize("fp-contract=off")))
+#endif
+#ifdef OR_TRI_CONTRACT
+__attribute__((optimize("fp-contract=fast")))
 #endif
 float or_tri_intersect(or_vec3 o, or_vec3 ray, const or_vec3* verts, const or_tri* t)
 {
     or_vec3 v0 = verts[t->v0], v1 = verts[t->v1], v2 = verts[t->v2];
     or_vec3 e1 = vsub(v1, v0);
     or_vec3 e2 = vsub(v2, v0);
-    or_vec3 q = vcross(ray, e2);
-    float a = vdot(e1, q);
+    or_vec3 q = tcross(ray, e2);
+    float a = tdot(e1, q);
     if ((double)fabsf(a) < 0.00001) return OR_MAX_FLOAT;
     or_vec3 s = vdiv(vsub(o, v0), a);
-    or_vec3 r = vcross(s, e1);
-    float b0 = vdot(s, q);
-    float b1 = vdot(r, ray);
+    or_vec3 r = tcross(s, e1);
+    float b0 = tdot(s, q);
+    float b1 = tdot(r, ray);
     float b2 = 1.0f - b0 - b1;
     if (b0 < 0.0f) return OR_MAX_FLOAT;
     if (b1 < 0.0f) return OR_MAX_FLOAT;
     if (b2 < 0.0f) return OR_MAX_FLOAT;
-    return vdot(e2, r);
+    return tdot(e2, r);
 }
 
 /* BVH.h:51-83 rayAABBIntersect (IEEE division, NaN-propagating compare/swap) */

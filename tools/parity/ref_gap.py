@@ -119,7 +119,7 @@ def gap(ref, var, pix, prim_flip, prim_tri_flip=None):
     return out
 
 
-def run(name, tiles, threads, cache_dir, variants):
+def run(name, tiles, threads, cache_dir, variants, pairs=()):
     cfg = WORKLOADS[name]
     osc, cam_kw = load_scene(cfg["scene"], cache_dir)
     w, h, spp, bounces = cfg["width"], cfg["height"], cfg["spp"], cfg["bounces"]
@@ -130,9 +130,11 @@ def run(name, tiles, threads, cache_dir, variants):
     t_ref = time.time() - t0
     rows = {}
     tri0, t0b = primary_hits(osc, ocam, w, pix, None)
+    imgs = {}
     for v in variants:
         t0 = time.time()
         img, _ = oracle.render(osc, ocam, w, h, spp, bounces, 0, 1234, pixels=pix, threads=threads, variant=v)
+        imgs[v] = img
         tri1, t1b = primary_hits(osc, ocam, w, pix, v)
         flip = (tri0 != tri1) | (t0b != t1b)
         rows[v] = dict(gap(ref, img, pix, flip, tri0 != tri1), seconds=round(time.time() - t0, 2))
@@ -147,8 +149,24 @@ def run(name, tiles, threads, cache_dir, variants):
                   name, v, r["rmse_tonemapped"], r["rmse_tonemapped_no_primary_triangle_flips"], r["primary_triangle_flips"],
                   r["rmse_tonemapped_no_primary_flips"], r["primary_hit_flips"], r["max_abs_tonemapped"],
                   r["pixels_differing_fp32"], r["pixels"]), flush=True)
+    # variant against variant (e.g. the two contraction shapes of triIntersect: how much the image depends on
+    # WHICH product a compiler fuses, not only on whether it fuses)
+    prow = {}
+    for a, b in pairs:
+        if a not in imgs or b not in imgs:
+            continue
+        ta, tab = primary_hits(osc, ocam, w, pix, a)
+        tb, tbb = primary_hits(osc, ocam, w, pix, b)
+        r = gap(imgs[a], imgs[b], pix, (ta != tb) | (tab != tbb), ta != tb)
+        prow["%s:%s" % (a, b)] = r
+        print("%s %s vs %s rmse %.3e (%.3e without %d primary triangle changes)  differing %d / %d pixels  "
+              "bit-identical %s" % (name, a, b, r["rmse_tonemapped"], r["rmse_tonemapped_no_primary_triangle_flips"],
+                                    r["primary_triangle_flips"], r["pixels_differing_fp32"], r["pixels"],
+                                    bool(np.array_equal(imgs[a].reshape(-1, 3)[pix], imgs[b].reshape(-1, 3)[pix]))),
+              flush=True)
     return {"workload": "%s %s %dx%d %dspp depth %d, every %d-th 8x8 tile (%d pixels)" % (
-        name, cfg["scene"], w, h, spp, bounces, stride, len(pix)), "oracle_seconds": round(t_ref, 2), "variants": rows}
+        name, cfg["scene"], w, h, spp, bounces, stride, len(pix)), "oracle_seconds": round(t_ref, 2), "variants": rows,
+        "pairs": prow}
 
 
 def main():
@@ -159,6 +177,7 @@ def main():
     ap.add_argument("--variants", default=",".join(oracle.VARIANTS))
     ap.add_argument("--workloads", default="C2,C3")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--pairs", default="", help="variant:variant,... compared with each other")
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
     os.makedirs(args.cache_dir, exist_ok=True)
@@ -166,7 +185,8 @@ def main():
     out = {"tool": "tools/parity/ref_gap.py", "threshold_north_star": 1e-4, "results": {}}
     for name in args.workloads.split(","):
         tiles = args.tiles_c2 if name == "C2" else args.tiles_c3
-        out["results"][name] = run(name, tiles, args.threads, args.cache_dir, variants)
+        pairs = [tuple(x.split(":")) for x in args.pairs.split(",") if x]
+        out["results"][name] = run(name, tiles, args.threads, args.cache_dir, variants, pairs)
     if args.json:
         with open(args.json, "w") as fh:
             json.dump(out, fh, indent=1)
