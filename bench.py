@@ -198,6 +198,20 @@ def roofline(counts, kms, W, H, args, world):
                                   "kernel_ms_profiled": tj.get("kernel_ms")}
         if tj.get("binding"):
             roof["binding"] = tj["binding"]
+        dr = tj.get("dram_requests")
+        if dr:
+            roof["hbm_counter"] = {
+                "counters": "TCC_EA0_RDREQ_DRAM_sum / TCC_EA0_WRREQ_DRAM_sum (rocprofv3, one --pmc pass)",
+                "rdreq_dram": dr["rdreq_dram"], "rdreq": dr["rdreq"], "wrreq_dram": dr["wrreq_dram"], "wrreq": dr["wrreq"],
+                "dram_share_of_memory_side_requests": round((dr["rdreq_dram"] + dr["wrreq_dram"]) /
+                                                            max(dr["rdreq"] + dr["wrreq"], 1), 4),
+                "separates_infinity_cache_hits": False,
+                "hbm_traffic": None, "hbm_frac": None,
+                "calibration": "profiles/r05_dram/dram_table.txt",
+                "note": "on a 32-MiB Infinity-Cache-resident table the DRAM-request counters equal the memory-side "
+                        "request counters (every L2 miss is 'destined for DRAM' whether the Infinity Cache or HBM "
+                        "serves it); no counter on this pool separates them, so HBM bytes proper are unmeasured "
+                        "and frac stays an upper bound"}
     return roof
 
 

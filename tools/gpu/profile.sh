@@ -9,6 +9,7 @@ B="python3 bench.py --no-cpu-baseline ${BENCH_ARGS}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- \
     $B --steps 2 --warmup 1 > $OUT/bench_ktrace.json 2> $OUT/bench_ktrace.err || { echo ktrace-fail > $OUT/done.txt; exit 1; }
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
+           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum" \
            "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD" \
            "SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" "TD_TD_BUSY_sum TD_TC_STALL_sum" \

@@ -59,6 +59,11 @@ if "GRBM_GUI_ACTIVE" in c:
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
         b["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
     out["binding"] = b
+if "TCC_EA0_RDREQ_DRAM_sum" in c:
+    # the DRAM-request counters (profiles/r05_dram: they equal the memory-side request counters on an
+    # Infinity-Cache-resident table, i.e. they count Infinity-Cache hits -- not an HBM measurement)
+    out["dram_requests"] = {"rdreq": int(c.get("TCC_EA0_RDREQ_sum", 0)), "rdreq_dram": int(c["TCC_EA0_RDREQ_DRAM_sum"]),
+                            "wrreq": int(c.get("TCC_EA0_WRREQ_sum", 0)), "wrreq_dram": int(c.get("TCC_EA0_WRREQ_DRAM_sum", 0))}
 # one entry per (config, source hash): a new measurement replaces the entry of its config
 path = os.path.join(ROOT, "profiles", "traffic.json")
 try:
