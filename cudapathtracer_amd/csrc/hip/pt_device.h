@@ -877,10 +877,13 @@ template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = 
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
-                                           const Setup& setup = Setup())
+                                           const Setup& setup = Setup(), bool active = true)
 {
-    const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 1);
-    const bool leaf = leaf4_pending(w);
+    // active = false (kCoop: the step runs wave-wide): a bystander lane visits, tests and pops nothing and
+    // keeps its walk state (a lane waiting to shade holds its hit there); it only takes its part in the
+    // cooperative fetch instructions
+    const bool visit = active && (w.node != kNone) && (w.lsp <= kLeafRing - 1);
+    const bool leaf = active && leaf4_pending(w);
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
     // (slots < 2^23, see kLeafBits: a full-rate 24-bit multiply; the slot is formed unconditionally
     // and selected, no branch)
@@ -940,7 +943,10 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             const uint32_t ncoop = min((uint32_t)__popcll(vm), kCoopSlots);   // (wave-uniform)
             if (coop) S.coop_idx[(cslot % 9u) * (uint32_t)kCoop + cslot / 9u] = nidx;
             const uint32_t lane = __lane_id();
-            const uint32_t g = (lane * 37u) >> 8, c = lane - g * 7u;   // lane / 7, lane % 7 (lane < 64)
+            // lane / 7 and lane % 7 (lane < 64), except lane 63 (no node of its own in a 9-node instruction):
+            // g = 8, c = 7 -- it fetches the 16-B pad of slot 8's node (same 128-B line, a valid address) into
+            // its own 16 B of the row, which nothing reads; so every lane's offset is a plain select
+            const uint32_t g = min((lane * 37u) >> 8, 8u), c = lane - g * 7u;
             uint32_t ids[4];
             if constexpr (kCoop == 1) {
                 ids[0] = S.coop_idx[g];
@@ -953,11 +959,10 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             }
 #pragma unroll
             for (int i = 0; i < kCoop; ++i) {
-                // lanes of no slot, and lane 63 always (g = 9: no node of this instruction; its index words
-                // were never written), read out of range: nothing is fetched, their 16 B of the instruction's
-                // 1-KiB staging row receive zeros nobody reads
+                // lanes of no slot read out of range: nothing is fetched, their 16 B of the instruction's 1-KiB
+                // staging row receive zeros nobody reads
                 const uint32_t j = 9u * (uint32_t)i + g;
-                const uint32_t off = (g < 9u && j < ncoop) ? ids[i] * 128u + c * 16u : 0x80000000u;
+                const uint32_t off = (j < ncoop) ? ids[i] * 128u + c * 16u : 0x80000000u;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(nrs, (__attribute__((address_space(3))) void*)(S.coop_stage + 1024 * i),
                                                          16, off, 0, 0, 0);
             }
@@ -1015,7 +1020,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         }
     }
     if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
-    advance4(w, S, cull_rel, node_mask);
+    if (kCoop == 0 || active) advance4(w, S, cull_rel, node_mask);
     if (kAnyHit && w.best_t <= w.occ) return false;
     return w.node != kNone || leaf4_pending(w);
 }

@@ -2131,10 +2131,17 @@ __device__ __forceinline__ void wf_main(const Args& a)
                 if (noleaf) ++itc[4];
                 if (noleaf && deep == 0u) ++itc[5];
             }
-            if (state == ST_TRACE) {
+            if constexpr (kCoop > 0) {
+                // the cooperative fetch's LDS-DMA instructions need every lane of the wave (a lane fetches a
+                // chunk of another lane's node): the step runs wave-wide, lanes not tracing as bystanders
+                const bool tr = state == ST_TRACE;
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, true, kCoop, kHead>(
+                    w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt, NoSetup(), tr);
+                if (tr && !more) state = ST_WALKED;
+            } else if (state == ST_TRACE) {
                 // (the culling factor as the literal it always is: a kernel argument here was a scalar
                 // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
-                const bool more = walk4_step<kCount, true, NoSetup, kHead, (kCoop > 0) || !kLdsWalk, kCoop, kHead>(
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk>(
                     w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
