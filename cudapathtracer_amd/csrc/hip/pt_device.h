@@ -767,7 +767,7 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 template <bool kCount>
 __device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX, const float4& NY, const float4& FY,
                                        const float4& NZ, const float4& FZ, const uint4& ch, const Stack4& S,
-                                       float cull_rel, uint32_t node_mask, Counters& cnt)
+                                       float cull_rel, uint32_t node_mask, Counters& cnt, uint32_t* second = nullptr)
 {
     const float lim = w.best_t * cull_rel;
     // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
@@ -818,6 +818,7 @@ __device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX
         if (k1 != kNone) push4<kCount>(w, S, k1, cnt);
     }
     w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
+    if (second) *second = (k1 != kNone) ? (k1 & node_mask) : kNone;   // (the stack's new top: visited next after k0's subtree)
 }
 // After a step: take the next queued leaf entry when the pending one is done, and pop the next stack
 // entry not culled by the best hit when there is no node to visit.
@@ -872,8 +873,11 @@ struct NoSetup {
 // without one), so the triangle test waits for the triangle only.
 // kCoopTop (with kCoop): lanes at a node of the LDS top read it there (no fetch); the cooperative slots go to
 // the lanes at deeper nodes (integrator 1, whose walk serves about half its visits from the top).
+// kPrefetch (experiment): after the step, each lane that pushed a second-nearest inner child fetches one word of
+// that node's line by LDS-DMA into a scratch row (no register, nothing waits for it until the next step's node
+// wait), so that the line is in L2 when the walk pops it.
 template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit,
-          int kCoop = 0, bool kCoopTop = false>
+          int kCoop = 0, bool kCoopTop = false, bool kPrefetch = false>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
@@ -1019,8 +1023,14 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
             ch = lds_u4a(mb + 96u);
         }
     }
-    if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
+    uint32_t second = kNone;
+    if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt, kPrefetch ? &second : nullptr);
     if (kCoop == 0 || active) advance4(w, S, cull_rel, node_mask);
+    if constexpr (kPrefetch) {
+        if (second != kNone)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(nrs, (__attribute__((address_space(3))) void*)S.coop_idx, 4,
+                                                     second * 128u, 0, 0, 0);
+    }
     if (kAnyHit && w.best_t <= w.occ) return false;
     return w.node != kNone || leaf4_pending(w);
 }

@@ -2021,7 +2021,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
 // The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
 // kLdsWalk: walk steps read the staged top from LDS (integrator 1 always; integrator 0 when the LDS
 // top holds the whole tree) instead of issuing every node's loads to memory.
-template <bool kCount, bool kHead, bool kLdsWalk = kHead, int kCoop = 0>
+template <bool kCount, bool kHead, bool kLdsWalk = kHead, int kCoop = 0, bool kPrefetch = false>
 __device__ __forceinline__ void wf_main(const Args& a)
 {
     extern __shared__ uint32_t lds_wf[];
@@ -2090,7 +2090,7 @@ __device__ __forceinline__ void wf_main(const Args& a)
     }
     S.top = reinterpret_cast<const char*>(ltop);
     S.ntop = a.top_nodes;
-    if constexpr (kCoop > 0) {   // after the top: per wave the index table (256 B) and kCoop staging rows of 1 KiB
+    if constexpr (kCoop > 0 || kPrefetch) {   // after the top: per wave the index table (256 B) and kCoop staging rows of 1 KiB
         char* const cbase = reinterpret_cast<char*>(ltop) + a.top_nodes * kTopNodeBytes;
         const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         char* const wb = cbase + wv * kCoopWaveBytes<kCoop>;
@@ -2141,7 +2141,7 @@ __device__ __forceinline__ void wf_main(const Args& a)
             } else if (state == ST_TRACE) {
                 // (the culling factor as the literal it always is: a kernel argument here was a scalar
                 // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
-                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk>(
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk, 0, false, kPrefetch>(
                     w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
@@ -2228,10 +2228,10 @@ __device__ __forceinline__ void wf_main(const Args& a)
     }
 }
 
-template <bool kCount, int kMinWaves, bool kLdsWalk = false, int kCoop = 0>
+template <bool kCount, int kMinWaves, bool kLdsWalk = false, int kCoop = 0, bool kPrefetch = false>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
-    wf_main<kCount, false, kLdsWalk, kCoop>(a);
+    wf_main<kCount, false, kLdsWalk, kCoop, kPrefetch>(a);
 }
 
 // integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the wavefront state machine
@@ -2473,6 +2473,7 @@ struct pt_ctx {
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
     int wf_coop = 0;                // integrator 0: cooperative node fetch, LDS-DMA instructions per step (PT_WF_COOP: 0/1/2/4)
     int head_coop = 0;              // integrator 1: the same (PT_HEAD_COOP: 0, 1 at 5 waves/SIMD, 2 at 4)
+    bool wf_prefetch = false;       // integrator 0: prefetch the pushed second-nearest child's line (PT_WF_PREFETCH)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
     int wf_tail_chunks = 6;         // chunks of each tail pixel (PT_WF_TAIL_CHUNKS; 1 = no tail split)
     double wf_tail_px = 1.5;        // tail pixels per resident lane (PT_WF_TAIL_PX; round 2 re-sweep after the
@@ -2706,6 +2707,7 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
         }
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
+        if (const char* e = getenv("PT_WF_PREFETCH")) c->wf_prefetch = atoi(e) != 0;
         if (const char* e = getenv("PT_HEAD_COOP")) {
             const int v = atoi(e);
             c->head_coop = (v == 1 || v == 2) ? v : 0;
@@ -3173,8 +3175,9 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         // (the cooperative fetch: integrator 0's memory walk only, not the counting variant, which keeps the
         // per-lane form -- the node visits are the same)
         const int coop = !count ? (head ? c->head_coop : c->wf_coop) : 0;
+        const bool prefetch = !count && !head && coop == 0 && c->wf_prefetch;
         const size_t coop_bytes = coop == 1 ? 4 * (size_t)kCoopWaveBytes<1> : coop == 2 ? 4 * (size_t)kCoopWaveBytes<2>
-                                : coop == 4 ? 4 * (size_t)kCoopWaveBytes<4> : 0;
+                                : coop == 4 ? 4 * (size_t)kCoopWaveBytes<4> : prefetch ? 4 * (size_t)kCoopWaveBytes<0> : 0;
         const size_t lds_fixed = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
                                  kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0) + coop_bytes;
         {   // as many top nodes as leave every block of a CU its LDS (granted in 1280-B granules): integrator 1's
@@ -3374,6 +3377,7 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5 && lds_tree) hipLaunchKernelGGL((render_unidir_wf<false, 5, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
+        else if (prefetch && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 0, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (coop == 1 && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 1>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (coop == 2 && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 2>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (coop == 4 && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<false, 4, false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
