@@ -721,10 +721,6 @@ struct Stack4 {
     uint32_t stride;
     const char* top = nullptr;   // LDS copy of BVH4 nodes 0..ntop-1 (kTopNodeBytes each), or none
     uint32_t ntop = 0;
-    // cooperative node fetch (walk4_step<..., kCoop>): this wave's index table (64 words) and staging
-    // (kCoop x 1 KiB: 9 nodes of kTopNodeBytes + 16 B per LDS-DMA wave-instruction), wave-uniform
-    uint32_t* coop_idx = nullptr;
-    char* coop_stage = nullptr;
     __device__ __forceinline__ uint32_t* spill() const
     {
         return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spill_base) + ((*lane_off & off_mask) >> off_shift));
@@ -767,7 +763,7 @@ __device__ __forceinline__ uint32_t pop4(W4& w, const Stack4& S)
 template <bool kCount>
 __device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX, const float4& NY, const float4& FY,
                                        const float4& NZ, const float4& FZ, const uint4& ch, const Stack4& S,
-                                       float cull_rel, uint32_t node_mask, Counters& cnt, uint32_t* second = nullptr)
+                                       float cull_rel, uint32_t node_mask, Counters& cnt)
 {
     const float lim = w.best_t * cull_rel;
     // empty slots hold a box no ray enters (accel_build.cpp), so all four tests run unguarded
@@ -818,7 +814,6 @@ __device__ __forceinline__ void visit4(W4& w, const float4& NX, const float4& FX
         if (k1 != kNone) push4<kCount>(w, S, k1, cnt);
     }
     w.node = (k0 != kNone) ? (k0 & node_mask) : kNone;
-    if (second) *second = (k1 != kNone) ? (k1 & node_mask) : kNone;   // (the stack's new top: visited next after k0's subtree)
 }
 // After a step: take the next queued leaf entry when the pending one is done, and pop the next stack
 // entry not culled by the best hit when there is no node to visit.
@@ -862,32 +857,14 @@ struct NoSetup {
 // always read from memory, not from the LDS top (the top's hot lines hit L2): C3 +1.5% (5630 -> 5713,
 // same box, alternated, profiles/r03_uni).  Integrator 1 (kAnyHit) keeps the LDS top: bound by bytes, it
 // lost 2.7% this way.
-// kCoop > 0 (integrator 0's uniform walk only; VERDICT r04 item 1, the node-gather probe's `coop` form):
-// the first 9 * kCoop visiting lanes of the wave (by lane order) do not load their node themselves.  They
-// publish the node index in the wave's LDS index table; then every lane takes part in kCoop LDS-DMA
-// wave-instructions (buffer_load_dwordx4 ... lds), in which 7 lanes fetch the 7 used 16-B chunks of one
-// node (lox, loy, loz, hix, hiy, hiz, child words): 9 nodes per instruction, one L1 lookup per node
-// instead of seven.  After the round trip the lane reads its node's planes from the staging copy exactly
-// as from the LDS top (same 112-B layout).  Visiting lanes beyond the 9 * kCoop slots load their node
-// per lane as before.  Every load is still issued unconditionally (out-of-range offsets for lanes
-// without one), so the triangle test waits for the triangle only.
-// kCoopTop (with kCoop): lanes at a node of the LDS top read it there (no fetch); the cooperative slots go to
-// the lanes at deeper nodes (integrator 1, whose walk serves about half its visits from the top).
-// kPrefetch (experiment): after the step, each lane that pushed a second-nearest inner child fetches one word of
-// that node's line by LDS-DMA into a scratch row (no register, nothing waits for it until the next step's node
-// wait), so that the line is in L2 when the walk pops it.
-template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit,
-          int kCoop = 0, bool kCoopTop = false, bool kPrefetch = false>
+template <bool kCount, bool kTop = false, class Setup = NoSetup, bool kAnyHit = false, bool kUniform = !kAnyHit>
 __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __restrict__ nodes,
                                            const DTri* __restrict__ tris, const Stack4& S, float cull_rel,
                                            float cull_abs, uint32_t node_mask, Counters& cnt,
-                                           const Setup& setup = Setup(), bool active = true)
+                                           const Setup& setup = Setup())
 {
-    // active = false (kCoop: the step runs wave-wide): a bystander lane visits, tests and pops nothing and
-    // keeps its walk state (a lane waiting to shade holds its hit there); it only takes its part in the
-    // cooperative fetch instructions
-    const bool visit = active && (w.node != kNone) && (w.lsp <= kLeafRing - 1);
-    const bool leaf = active && leaf4_pending(w);
+    const bool visit = (w.node != kNone) && (w.lsp <= kLeafRing - 1);
+    const bool leaf = leaf4_pending(w);
     // 32-bit byte offsets from the (uniform) array bases: pt_create keeps both arrays < 4 GiB
     // (slots < 2^23, see kLeafBits: a full-rate 24-bit multiply; the slot is formed unconditionally
     // and selected, no branch)
@@ -915,24 +892,8 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     const uint32_t nidx = visit ? w.node : 0u;
     float4 NX, FX, NY, FY, NZ, FZ;
     uint4 ch;
-    static_assert(kCoop == 0 || kCoop == 1 || kCoop == 2 || kCoop == 4, "kCoop: 1, 2 or 4 LDS-DMA instructions");
-    static_assert(kCoop == 0 || kUniform, "the cooperative fetch is a form of the uniform step");
-    constexpr uint32_t kCoopSlots = 9u * (uint32_t)kCoop;
-    uint32_t cslot = 0;   // (kCoop) this lane's slot among the wave's visiting lanes
-    bool coop = false;    // (kCoop) this lane's node comes through the LDS staging
-    bool topl = false;    // (kCoopTop) this lane's node is read from the LDS top
     if constexpr (kUniform) {
-        bool own = visit;   // this lane loads its node itself
-        uint64_t vm = 0;
-        if constexpr (kCoop > 0) {
-            const bool deep = visit && (!kCoopTop || nidx >= S.ntop);
-            topl = kCoopTop && visit && !deep;
-            vm = __ballot(deep);
-            cslot = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
-            coop = deep && cslot < kCoopSlots;
-            own = deep && !coop;
-        }
-        const uint32_t nb = own ? nidx * 128u : 0x80000000u;
+        const uint32_t nb = visit ? nidx * 128u : 0x80000000u;
         auto bl = [&](uint32_t off) {
             const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(nrs, off, 0, 0));
             return make_float4(v.x, v.y, v.z, v.w);
@@ -941,36 +902,6 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         NX = bl(ox); FX = bl(ox ^ 48u); NY = bl(oy); FY = bl(oy ^ 80u); NZ = bl(oz); FZ = bl(oz ^ 112u);
         const float4 c4 = bl(nb + 96u);
         ch = make_uint4(__float_as_uint(c4.x), __float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w));
-        if constexpr (kCoop > 0) {
-            // slot s's node index at word (s % 9) * kCoop + s / 9: lane L, which fetches chunk L % 7 of the
-            // node in slot 9i + L / 7 in instruction i, reads its kCoop indices as consecutive words
-            const uint32_t ncoop = min((uint32_t)__popcll(vm), kCoopSlots);   // (wave-uniform)
-            if (coop) S.coop_idx[(cslot % 9u) * (uint32_t)kCoop + cslot / 9u] = nidx;
-            const uint32_t lane = __lane_id();
-            // lane / 7 and lane % 7 (lane < 64), except lane 63 (no node of its own in a 9-node instruction):
-            // g = 8, c = 7 -- it fetches the 16-B pad of slot 8's node (same 128-B line, a valid address) into
-            // its own 16 B of the row, which nothing reads; so every lane's offset is a plain select
-            const uint32_t g = min((lane * 37u) >> 8, 8u), c = lane - g * 7u;
-            uint32_t ids[4];
-            if constexpr (kCoop == 1) {
-                ids[0] = S.coop_idx[g];
-            } else if constexpr (kCoop == 2) {
-                const uint2 v = *reinterpret_cast<const uint2*>(S.coop_idx + 2u * g);
-                ids[0] = v.x; ids[1] = v.y;
-            } else {
-                const uint4 v = *reinterpret_cast<const uint4*>(S.coop_idx + 4u * g);
-                ids[0] = v.x; ids[1] = v.y; ids[2] = v.z; ids[3] = v.w;
-            }
-#pragma unroll
-            for (int i = 0; i < kCoop; ++i) {
-                // lanes of no slot read out of range: nothing is fetched, their 16 B of the instruction's 1-KiB
-                // staging row receive zeros nobody reads
-                const uint32_t j = 9u * (uint32_t)i + g;
-                const uint32_t off = (j < ncoop) ? ids[i] * 128u + c * 16u : 0x80000000u;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(nrs, (__attribute__((address_space(3))) void*)(S.coop_stage + 1024 * i),
-                                                         16, off, 0, 0, 0);
-            }
-        }
     } else {
     // Every lane reads the LDS copy first (a deep node's lane reads node 0: a broadcast), then the
     // deep nodes' lanes overwrite it with their global loads -- in this order, because the loads
@@ -997,7 +928,7 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
     }
     setup(w);
     pin_use(A); pin_use(B); pin_use1(e2z);   // (the node's fields feed unconditional tests: no pin needed)
-    if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop && (!kUniform || kCoopTop)) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
+    if (kCount) { if (visit) ++cnt.nodes; if (visit && nidx < S.ntop && !kUniform) ++cnt.top; if (leaf) { ++cnt.tris; ++cnt.leaf_steps; } }
     if (leaf) {
         const float t = tri_hit_pk(f2{o.x, o.y}, o.z, f2{d.x, d.y}, d.z, A, B, e2z);
         const uint32_t lslot = leaf4_slot(w);   // (recomputed here: one register less across the loads)
@@ -1011,26 +942,8 @@ __device__ __forceinline__ bool walk4_step(W4& w, V3 o, V3 d, const DNode4* __re
         }
         w.leaf &= w.leaf - 1u;   // that leaf is done
     }
-    if constexpr (kCoop > 0) {
-        // the staging rows are written by the LDS-DMA instructions: their data has landed once vmcnt is 0
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (coop || topl) {   // (over the per-lane loads' out-of-range zeros: same registers)
-            const uint32_t mb = coop ? lds_addr(S.coop_stage) + cslot * kTopNodeBytes + (cslot / 9u) * 16u
-                                     : lds_addr(S.top) + __umul24(nidx, kTopNodeBytes);
-            NX = lds_f4a(mb + w.nx); FX = lds_f4a(vsub_u32(mb, w.nx) + 48u);
-            NY = lds_f4a(mb + w.ny); FY = lds_f4a(vsub_u32(mb, w.ny) + 80u);
-            NZ = lds_f4a(mb + w.nz); FZ = lds_f4a(vsub_u32(mb, w.nz) + 112u);
-            ch = lds_u4a(mb + 96u);
-        }
-    }
-    uint32_t second = kNone;
-    if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt, kPrefetch ? &second : nullptr);
-    if (kCoop == 0 || active) advance4(w, S, cull_rel, node_mask);
-    if constexpr (kPrefetch) {
-        if (second != kNone)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(nrs, (__attribute__((address_space(3))) void*)S.coop_idx, 4,
-                                                     second * 128u, 0, 0, 0);
-    }
+    if (visit) visit4<kCount>(w, NX, FX, NY, FY, NZ, FZ, ch, S, cull_rel, node_mask, cnt);
+    advance4(w, S, cull_rel, node_mask);
     if (kAnyHit && w.best_t <= w.occ) return false;
     return w.node != kNone || leaf4_pending(w);
 }

@@ -1518,9 +1518,6 @@ enum : int {
 // 4-7 visibility bits, 8-11 the connections that need a ray
 enum : uint32_t { HS_T1 = 0, HS_T2 = 1, HS_T3 = 2, HS_SH = 3 };
 constexpr int kHeadLdsLightBytes = (int)kLdsLights * 16;   // per staged light: its normal and material
-// cooperative node fetch (walk4_step<..., kCoop>): per wave a 64-word index table + kCoop 1-KiB staging rows
-template <int kCoop>
-constexpr uint32_t kCoopWaveBytes = 256u + 1024u * (uint32_t)kCoop;
 
 // The geometric factors of one HEAD sample's connections (kernel.cu:353-412): G1 = geo_term of the
 // light subpath edge x1-x0, G3 = of the camera edge x3-x2, Gc[k] = the connection term of (i, j),
@@ -2021,7 +2018,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
 // The wavefront kernel's body, shared by both integrators (kHead: integrator 1, shade_lane_head).
 // kLdsWalk: walk steps read the staged top from LDS (integrator 1 always; integrator 0 when the LDS
 // top holds the whole tree) instead of issuing every node's loads to memory.
-template <bool kCount, bool kHead, bool kLdsWalk = kHead, int kCoop = 0, bool kPrefetch = false>
+template <bool kCount, bool kHead, bool kLdsWalk = kHead>
 __device__ __forceinline__ void wf_main(const Args& a)
 {
     extern __shared__ uint32_t lds_wf[];
@@ -2090,13 +2087,6 @@ __device__ __forceinline__ void wf_main(const Args& a)
     }
     S.top = reinterpret_cast<const char*>(ltop);
     S.ntop = a.top_nodes;
-    if constexpr (kCoop > 0 || kPrefetch) {   // after the top: per wave the index table (256 B) and kCoop staging rows of 1 KiB
-        char* const cbase = reinterpret_cast<char*>(ltop) + a.top_nodes * kTopNodeBytes;
-        const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        char* const wb = cbase + wv * kCoopWaveBytes<kCoop>;
-        S.coop_idx = reinterpret_cast<uint32_t*>(wb);
-        S.coop_stage = wb + 256;
-    }
     __syncthreads();
     const uint32_t nlanes = gridDim.x * blockDim.x, wave_id = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (a.lane_times && lane == 0) a.lane_times[nlanes + wave_id] = wall_clock64();
@@ -2131,17 +2121,10 @@ __device__ __forceinline__ void wf_main(const Args& a)
                 if (noleaf) ++itc[4];
                 if (noleaf && deep == 0u) ++itc[5];
             }
-            if constexpr (kCoop > 0) {
-                // the cooperative fetch's LDS-DMA instructions need every lane of the wave (a lane fetches a
-                // chunk of another lane's node): the step runs wave-wide, lanes not tracing as bystanders
-                const bool tr = state == ST_TRACE;
-                const bool more = walk4_step<kCount, true, NoSetup, kHead, true, kCoop, kHead>(
-                    w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt, NoSetup(), tr);
-                if (tr && !more) state = ST_WALKED;
-            } else if (state == ST_TRACE) {
+            if (state == ST_TRACE) {
                 // (the culling factor as the literal it always is: a kernel argument here was a scalar
                 // load and wait on every step's chain, the compiler rematerialising it for want of SGPRs)
-                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk, 0, false, kPrefetch>(
+                const bool more = walk4_step<kCount, true, NoSetup, kHead, !kLdsWalk>(
                     w, ro, rd, a.nodes4, a.acc_tris, S, kCullRel, a.cull_abs, a.node_mask, cnt);
                 if (kCount) ++steps;
                 if (kCount && !more) {   // walk length histogram, log2 buckets
@@ -2228,17 +2211,17 @@ __device__ __forceinline__ void wf_main(const Args& a)
     }
 }
 
-template <bool kCount, int kMinWaves, bool kLdsWalk = false, int kCoop = 0, bool kPrefetch = false>
+template <bool kCount, int kMinWaves, bool kLdsWalk = false>
 __global__ __launch_bounds__(256, kMinWaves) void render_unidir_wf(Args a)
 {
-    wf_main<kCount, false, kLdsWalk, kCoop, kPrefetch>(a);
+    wf_main<kCount, false, kLdsWalk>(a);
 }
 
 // integrator 1 (radianceAlongSingleStep, kernel.cu:217-415) on the wavefront state machine
-template <bool kCount, int kMinWaves, int kCoop = 0>
+template <bool kCount, int kMinWaves>
 __global__ __launch_bounds__(256, kMinWaves) void render_head_wf(Args a)
 {
-    wf_main<kCount, true, true, kCoop>(a);
+    wf_main<kCount, true>(a);
 }
 
 // ------------------------------------------------------------------ output step
@@ -2471,9 +2454,6 @@ struct pt_ctx {
                                     // (PT_WF_ROOT_FIRST; C3 1/2/3/4/6: 5331/5417/5461/5509/5406)
     uint32_t wf_waves_per_cu = 16;
     int wf_min_waves = 5;           // register budget of the wavefront kernel (PT_WF_MIN_WAVES: 4/5/6)
-    int wf_coop = 0;                // integrator 0: cooperative node fetch, LDS-DMA instructions per step (PT_WF_COOP: 0/1/2/4)
-    int head_coop = 0;              // integrator 1: the same (PT_HEAD_COOP: 0, 1 at 5 waves/SIMD, 2 at 4)
-    bool wf_prefetch = false;       // integrator 0: prefetch the pushed second-nearest child's line (PT_WF_PREFETCH)
     int wf_chunks = 0;              // sample chunks per pixel, 0 = automatic (PT_WF_CHUNKS)
     int wf_tail_chunks = 6;         // chunks of each tail pixel (PT_WF_TAIL_CHUNKS; 1 = no tail split)
     double wf_tail_px = 1.5;        // tail pixels per resident lane (PT_WF_TAIL_PX; round 2 re-sweep after the
@@ -2707,15 +2687,6 @@ pt_ctx* pt_create(const pt_scene* sc, int device, int* err)
             c->wf_min_waves = (v == 4 || v == 6) ? v : 5;
         }
         c->wf_waves_per_cu = 4u * (uint32_t)c->wf_min_waves;
-        if (const char* e = getenv("PT_WF_PREFETCH")) c->wf_prefetch = atoi(e) != 0;
-        if (const char* e = getenv("PT_HEAD_COOP")) {
-            const int v = atoi(e);
-            c->head_coop = (v == 1 || v == 2) ? v : 0;
-        }
-        if (const char* e = getenv("PT_WF_COOP")) {
-            const int v = atoi(e);
-            c->wf_coop = (v == 1 || v == 2 || v == 4) ? v : 0;
-        }
         if (const char* e = getenv("PT_WF_WAVES_PER_CU")) c->wf_waves_per_cu = (uint32_t)atoi(e);
         if (const char* e = getenv("PT_WF_CHUNKS")) c->wf_chunks = atoi(e);
         if (const char* e = getenv("PT_WF_TAIL_CHUNKS")) c->wf_tail_chunks = atoi(e);
@@ -3172,14 +3143,8 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         b.top_nodes = c->top_nodes;
         b.head = head ? 1u : 0u;
         const uint32_t wpc = (head && !count) ? 4u * (uint32_t)c->head_min_waves : c->wf_waves_per_cu;
-        // (the cooperative fetch: integrator 0's memory walk only, not the counting variant, which keeps the
-        // per-lane form -- the node visits are the same)
-        const int coop = !count ? (head ? c->head_coop : c->wf_coop) : 0;
-        const bool prefetch = !count && !head && coop == 0 && c->wf_prefetch;
-        const size_t coop_bytes = coop == 1 ? 4 * (size_t)kCoopWaveBytes<1> : coop == 2 ? 4 * (size_t)kCoopWaveBytes<2>
-                                : coop == 4 ? 4 * (size_t)kCoopWaveBytes<4> : prefetch ? 4 * (size_t)kCoopWaveBytes<0> : 0;
         const size_t lds_fixed = (size_t)kWaveLdsWords * 4 * 4 + 4 * sizeof(unsigned long long) + (kSections + kHist) * 4 +
-                                 kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0) + coop_bytes;
+                                 kProbeLdsBytes + (head ? (size_t)kHeadLdsLightBytes : 0);
         {   // as many top nodes as leave every block of a CU its LDS (granted in 1280-B granules): integrator 1's
             // staged light normals cost it one node at 5 blocks per CU (97 -> 96), which kept it at 4 blocks
             const uint32_t bpc = std::max(1u, wpc / 4u);
@@ -3367,8 +3332,6 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         split = b.ntail;
         if (head) {
             if (count) hipLaunchKernelGGL((render_head_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
-            else if (coop == 1 && c->head_min_waves == 5) hipLaunchKernelGGL((render_head_wf<false, 5, 1>), dim3(blocks), dim3(256), lds_wf, stream, b);
-            else if (coop == 2 && c->head_min_waves == 4) hipLaunchKernelGGL((render_head_wf<false, 4, 2>), dim3(blocks), dim3(256), lds_wf, stream, b);
             else if (c->head_min_waves == 4) hipLaunchKernelGGL((render_head_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
             else hipLaunchKernelGGL((render_head_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         }
@@ -3377,10 +3340,6 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
         else if (count) hipLaunchKernelGGL((render_unidir_wf<true, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 6) hipLaunchKernelGGL((render_unidir_wf<false, 6>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5 && lds_tree) hipLaunchKernelGGL((render_unidir_wf<false, 5, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
-        else if (prefetch && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 0, true>), dim3(blocks), dim3(256), lds_wf, stream, b);
-        else if (coop == 1 && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 1>), dim3(blocks), dim3(256), lds_wf, stream, b);
-        else if (coop == 2 && c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5, false, 2>), dim3(blocks), dim3(256), lds_wf, stream, b);
-        else if (coop == 4 && c->wf_min_waves == 4) hipLaunchKernelGGL((render_unidir_wf<false, 4, false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else if (c->wf_min_waves == 5) hipLaunchKernelGGL((render_unidir_wf<false, 5>), dim3(blocks), dim3(256), lds_wf, stream, b);
         else hipLaunchKernelGGL((render_unidir_wf<false, 4>), dim3(blocks), dim3(256), lds_wf, stream, b);
         HIP_TRY(hipGetLastError());

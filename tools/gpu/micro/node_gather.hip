@@ -145,6 +145,39 @@ __global__ __launch_bounds__(256) void lane_oor_form(const uint4* __restrict__ n
     out[g] = acc;
 }
 
+// Per-instruction cost probe (round 5): 7 loads per step of width W bytes (4: dword, 16: dwordx4), kAct lanes
+// active; kMask: the others exec-masked (true) or at an out-of-range buffer offset (false).  If the cost per
+// wave-step stays ~constant as kAct falls to 1, the memory pipe charges per wave-instruction (not per lane).
+template <int kAct, int kW, bool kMask>
+__global__ __launch_bounds__(256) void width_form(const uint4* __restrict__ nodes, uint32_t nn, uint32_t* out)
+{
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+    uint32_t idx = hash(g * 2654435761u + 7u) % nn, acc = 0;
+    const bool act = (int)lane < kAct;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(nodes), 0, 0x7fffff00, 0x00020000);
+    if (kMask && !act) { out[g] = 0; return; }
+    for (int s = 0; s < kSteps; ++s) {
+        const uint32_t nb = act ? idx * 128u : 0x80000000u;
+        uint32_t x = 0, last = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            if (kW == 16) {
+                const u4 w = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, nb + 16u * k, 0, 0));
+                x ^= w.x ^ w.y ^ w.z ^ w.w;
+                last = w.x;
+            } else {
+                const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rs, nb + 16u * k, 0, 0);
+                x ^= w;
+                last = w;
+            }
+        }
+        acc += x;
+        if (act) idx = (last ^ (lane * 0x9e3779b9u) ^ (uint32_t)s) % nn;
+    }
+    out[g] = acc;
+}
+
 template <class K>
 static double timeit(K kern, dim3 grid, size_t lds, const uint4* nodes, uint32_t nn, uint32_t* out)
 {
@@ -187,6 +220,13 @@ int main(int argc, char** argv)
         rs.push_back({"lane_oor 20 active", timeit(lane_oor_form<20>, grid, 0, nodes, nn, out), 20});
         rs.push_back({"lane 20 active", timeit(lane_form<20>, grid, 0, nodes, nn, out), 20});
         rs.push_back({"lane_oor 64 active", timeit(lane_oor_form<64>, grid, 0, nodes, nn, out), 64});
+        rs.push_back({"w16 oor 1 active", timeit(width_form<1, 16, false>, grid, 0, nodes, nn, out), 1});
+        rs.push_back({"w16 exec 1 active", timeit(width_form<1, 16, true>, grid, 0, nodes, nn, out), 1});
+        rs.push_back({"w16 oor 8 active", timeit(width_form<8, 16, false>, grid, 0, nodes, nn, out), 8});
+        rs.push_back({"w16 oor 40 active", timeit(width_form<40, 16, false>, grid, 0, nodes, nn, out), 40});
+        rs.push_back({"w4 oor 1 active", timeit(width_form<1, 4, false>, grid, 0, nodes, nn, out), 1});
+        rs.push_back({"w4 oor 40 active", timeit(width_form<40, 4, false>, grid, 0, nodes, nn, out), 40});
+        rs.push_back({"w4 oor 64 active", timeit(width_form<64, 4, false>, grid, 0, nodes, nn, out), 64});
         if (bpc == 4) {   // (32 KiB of staging per block: 4 blocks per CU)
             rs.push_back({"coop 64 active", timeit(coop_form<64>, grid, coop_lds, nodes, nn, out), 64});
             rs.push_back({"coop 40 active", timeit(coop_form<40>, grid, coop_lds, nodes, nn, out), 40});
