@@ -13,10 +13,18 @@ for c in ${CONFIGS:-C2 C5}; do
   [ "$PROF" = "0" ] && continue
   timeout -k 10 ${TLIM:-300} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/ktrace -o run -- \
       $B --no-cpu-baseline --no-count > $OUT/$c/bench_ktrace.json 2> $OUT/$c/bench_ktrace.err || { echo "ktrace-fail $c" > $OUT/done.txt; exit 1; }
-  for grp in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 ${TLIM:-300} rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/$c/pmc_$grp -o run -- \
+  # FULL_PMC=1: also the binding groups of tools/gpu/profile.sh and the DRAM-request pass (traffic.json's
+  # `binding` and `dram_requests` blocks)
+  GROUPS_=("FETCH_SIZE" "WRITE_SIZE")
+  [ "$FULL_PMC" = "1" ] && GROUPS_+=("TCC_HIT_sum TCC_MISS_sum" \
+      "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum" \
+      "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD" \
+      "TA_TA_BUSY_sum GRBM_GUI_ACTIVE" "TD_TD_BUSY_sum TD_TC_STALL_sum" "TCP_TOTAL_CACHE_ACCESSES_sum SQ_INSTS_VMEM_WR")
+  for grp in "${GROUPS_[@]}"; do
+    tag=$(echo $grp | cut -d' ' -f1)
+    timeout -k 10 ${TLIM:-300} rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/$c/pmc_$tag -o run -- \
         python3 bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline --no-count ${BENCH_ARGS} \
-        > $OUT/$c/bench_$grp.json 2> $OUT/$c/bench_$grp.err || { echo "pmc-fail $c $grp" > $OUT/done.txt; exit 1; }
+        > $OUT/$c/bench_$tag.json 2> $OUT/$c/bench_$tag.err || { echo "pmc-fail $c $tag" > $OUT/done.txt; exit 1; }
   done
 done
 echo ok > $OUT/done.txt

@@ -39,11 +39,19 @@ out = {
 }
 if "GRBM_GUI_ACTIVE" in c:
     cyc = c["GRBM_GUI_ACTIVE"] / 8.0     # summed over the 8 XCDs
-    b = {"limiter": "the walk's dependent memory round trips per ray (walk steps): the step's dependent VALU "
-                    "(deferred under the next fetch), its L1 lookups (-18%) and a sixth wave per SIMD each "
-                    "left the rate unchanged, fewer steps moved it (DESIGN.md 6, 10); TD busy counts requests "
-                    "in flight, VALU issue is about half its wave64 rate (0.5 wave64 instructions per SIMD-cycle)",
-         "cycles_per_launch": int(cyc)}
+    if cfg[:4] == [1024, 1024, 64, 8]:   # C2: the 32-triangle Cornell tree, held whole in LDS
+        lim = ("C2's tree (32 triangles) is read from LDS and every other record hits L2: not bytes -- the path "
+               "state held in registers removed 37-42% of the memory-side bytes for -0.8% (profiles/r04_c2_regstate); "
+               "the walk runs at SIMD utilisation ~0.39 (walk threshold 62, LDS round trips per step) and the f64 "
+               "shading pass carries most of the VALU, whose issue rate below is about half the wave64 ceiling; "
+               "TD_TC_STALL is the vector memory's share of cycles stalled on the record's L2 round trips (DESIGN.md 6)")
+    else:
+        lim = ("the walk's dependent memory round trips per ray (walk steps) and their latency: the step's dependent "
+               "VALU (deferred under the next fetch: +-0), its L1 lookups (-18%: +-0; -21% / -37% by the cooperative "
+               "fetch, which lengthens the chain: -7% / -16%, profiles/r05_coop) and a sixth wave per SIMD each left "
+               "the rate unchanged or lower, fewer steps moved it (DESIGN.md 6, 10); TD busy counts requests in "
+               "flight, VALU issue is about half its wave64 rate (0.5 wave64 instructions per SIMD-cycle)")
+    b = {"limiter": lim, "cycles_per_launch": int(cyc)}
     if "SQ_INSTS_VALU" in c:
         # wave64 VALU instructions per SIMD-cycle; the issue ceiling is 0.5 (a wave64 VALU instruction
         # issues over 2 cycles on CDNA4's SIMD-32, MI355X_MICROARCH.md "Wave scheduling")
