@@ -73,3 +73,24 @@ def test_committed_traffic_json_covers_the_bench_configs():
         e = bench.traffic_entry(path, cfg, sha)
         assert e is not None, cfg
         assert e["traffic_bytes_per_launch"] / (e["kernel_ms"] * 1e-3) / 1e9 <= bench.HBM_PEAK_GBS
+
+
+def test_hbm_counter_block_states_it_cannot_separate_infinity_cache_hits(tmp_path):
+    """with the DRAM-request counters recorded for the launch, the roofline carries them
+    beside the memory-side frac -- and says what the calibration (profiles/r05_dram) showed: they count the
+    Infinity Cache's hits too, so no HBM-only bytes or frac are claimed."""
+    sha = bench.kernel_source_sha256()
+    p = tmp_path / "t.json"
+    dr = {"rdreq": 2_097_356_374, "rdreq_dram": 2_097_356_374, "wrreq": 1_495_031_059, "wrreq_dram": 1_495_031_059}
+    p.write_text(json.dumps({"entries": [{"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha,
+                                          "traffic_bytes_per_launch": 351_000_000_000, "kernel_ms": 91.7,
+                                          "profile": "profiles/x", "dram_requests": dr}]}))
+    roof = bench.roofline(COUNTS, 90.5, 1920, 1080, _args(str(p)), 1)
+    h = roof["hbm_counter"]
+    assert h["separates_infinity_cache_hits"] is False
+    assert h["hbm_traffic"] is None and h["hbm_frac"] is None
+    assert h["dram_share_of_memory_side_requests"] == 1.0
+    assert os.path.exists(os.path.join(bench.ROOT, h["calibration"]))
+    # the committed C3 entry carries the counters
+    e = bench.traffic_entry(os.path.join(bench.ROOT, "profiles", "traffic.json"), [1920, 1080, 256, 3, 0, 1], sha)
+    assert e is not None and e["dram_requests"]["rdreq_dram"] == e["dram_requests"]["rdreq"]
