@@ -94,8 +94,8 @@ struct Args {
     uint32_t* pmemo;                // split slots: primary hit of tail slot t as one 64-bit word: lo = tri + 2
                                     // (0 = not yet), hi = t
     double* lbuf;                   // split slots: per-sample radiance, channel k of sample n of tail slot t
-                                    // at lbuf[(t * spp + n-1) * 3 + k] (a slot's samples contiguous: each
-                                    // lane fills whole lines with its own consecutive samples)
+                                    // at lbuf[((n-1) * ntail + t) * 3 + k] (sample-major: a wave of
+                                    // finalize_pixels reads 64 slots' sample n as 1.5 KB in a row)
     const float4* spheres;          // sphere primitives: center xyz, radius (hit ids num_tris + i)
     uint32_t num_spheres;
     uint32_t num_tris;
@@ -875,7 +875,8 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     uint32_t px, py;
     if (!unit_pixel(a, a.nwhole + t, &px, &py)) return;
     const size_t pix = out_pixel(a, px, py);
-    const double* L = a.lbuf + (size_t)t * a.spp * 3;
+    const double* L = a.lbuf + (size_t)t * 3;
+    const size_t stride = (size_t)a.ntail * 3;   // one sample of every slot
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
     // one sample: the six quotients by fn as one IEEE reciprocal + Markstein corrections (RN(x/fn)
     // for finite x clear of under/overflow, as in the render kernel's sample end) -- else the wave
@@ -894,17 +895,30 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
             m2 = x2 / fn + l2 / fn;
         }
     };
-    // eight samples' loads issued together (the lane's samples are contiguous: one dependent round
-    // trip per eight samples instead of per sample)
+    // eight samples' loads issued together, the next eight issued before these are consumed (a wave's
+    // loads of one sample are 64 consecutive slots: whole lines)
     int n = 1;
-    for (; n + 7 <= a.spp; n += 8, L += 24) {
-        double v[24];
+    double v[24];
+    if (n + 7 <= a.spp) {
 #pragma unroll
-        for (int k = 0; k < 24; ++k) v[k] = L[k];
+        for (int k = 0; k < 8; ++k) { v[3 * k] = L[k * stride]; v[3 * k + 1] = L[k * stride + 1]; v[3 * k + 2] = L[k * stride + 2]; }
+    }
+    for (; n + 7 <= a.spp; n += 8) {
+        L += 8 * stride;
+        double q[24];
+        const bool more = n + 15 <= a.spp;
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { q[3 * k] = L[k * stride]; q[3 * k + 1] = L[k * stride + 1]; q[3 * k + 2] = L[k * stride + 2]; }
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) step(n + k, v[3 * k], v[3 * k + 1], v[3 * k + 2]);
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < 24; ++k) v[k] = q[k];
+        }
     }
-    for (; n <= a.spp; ++n, L += 3) step(n, L[0], L[1], L[2]);
+    for (; n <= a.spp; ++n, L += stride) step(n, L[0], L[1], L[2]);
     float* o3 = a.out + pix * 3;
     o3[0] = (float)m0;
     o3[1] = (float)m1;
@@ -1261,7 +1275,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                     // split pixel: keep L_n, finalize_pixels forms the ordered mean
                     // (the slot is cell 8's last word, fetched with this sample's end: no dependent fetch
                     // before the stores)
-                    double* L = a.lbuf + ((size_t)c8.w * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
+                    double* L = a.lbuf + ((size_t)(uint32_t)(n - 1) * a.ntail + c8.w) * 3;
                     L[0] = acc.r;
                     L[1] = acc.g;
                     L[2] = acc.b;
@@ -1944,7 +1958,7 @@ __device__ __forceinline__ void shade_lane_head(const ColdRec& R, int lane, uint
                 R.st4(HW_M, dlo(m0), dhi(m0), dlo(mm1), dhi(mm1));
                 R.st2(HW_M + 4, dlo(mm2), dhi(mm2));
             } else {
-                double* Lb = a.lbuf + ((size_t)c13.y * (uint32_t)a.spp + (uint32_t)(n - 1)) * 3;
+                double* Lb = a.lbuf + ((size_t)(uint32_t)(n - 1) * a.ntail + c13.y) * 3;
                 Lb[0] = acc.r;
                 Lb[1] = acc.g;
                 Lb[2] = acc.b;
