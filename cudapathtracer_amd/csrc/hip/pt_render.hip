@@ -657,7 +657,10 @@ enum : int {
 };
 // CF_ACC0: the sample's accumulator is 0 (not yet written: the record's acc words are stale)
 enum : uint32_t { CF_LENS = 1, CF_HAVE = 2, CF_PRIMARY = 4, CF_OWNER = 8, CF_SHARE = 16, CF_MEMO = 32, CF_CAMC = 64,
-                  CF_ACC0 = 128, CF_SPLIT = 256 };
+                  CF_ACC0 = 128, CF_SPLIT = 256, CF_CHUNK0 = 512 };
+// CF_CHUNK0 (integrator 0): a split pixel's first chunk (samples 1..chunk_first(1)) keeps the running mean
+// itself, as a whole pixel does, and leaves it in its slot's sample-1 row of lbuf for finalize_pixels to
+// continue from.
 
 // Accessed as raw buffer loads/stores: one VGPR lane offset for the whole record and the cell
 // offset (w / 4) * stride in an SGPR, so no per-word 64-bit addresses are held across the phase.
@@ -877,7 +880,13 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     const size_t pix = out_pixel(a, px, py);
     const double* L = a.lbuf + (size_t)t * 3;
     const size_t stride = (size_t)a.ntail * 3;   // one sample of every slot
+    // integrator 0: chunk 0 left its running mean after samples 1..e0 in the sample-1 row (CF_CHUNK0);
+    // integrator 1 stores every sample (its chunk 0 keeping the mean measured -1% on the 1/8 shard)
+    const uint32_t nc = t < a.nmid ? a.chunks_mid : t >= a.ntail - a.nfin ? a.chunks_fin : a.chunks;
+    const uint32_t e0 = a.head ? 0u : chunk_first(a, 1u, nc);
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    if (e0 != 0u) { m0 = L[0]; m1 = L[1]; m2 = L[2]; }
+    L += (size_t)e0 * stride;
     // one sample: the six quotients by fn as one IEEE reciprocal + Markstein corrections (RN(x/fn)
     // for finite x clear of under/overflow, as in the render kernel's sample end) -- else the wave
     // divides
@@ -897,7 +906,7 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     };
     // eight samples' loads issued together, the next eight issued before these are consumed (a wave's
     // loads of one sample are 64 consecutive slots: whole lines)
-    int n = 1;
+    int n = (int)e0 + 1;
     double v[24];
     if (n + 7 <= a.spp) {
 #pragma unroll
@@ -1243,7 +1252,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                 const uint4 a2m0 = R.ld4(CW_ACC + 4);   // (acc.b, only when !CF_ACC0) and m0
                 const C3 acc = (fl & CF_ACC0) ? c3(0.0, 0.0, 0.0)
                                               : c3(dbl(a01.x, a01.y), dbl(a01.z, a01.w), dbl(a2m0.x, a2m0.y));
-                if (!(fl & CF_SPLIT)) {
+                if (!(fl & CF_SPLIT) || (fl & CF_CHUNK0)) {
                     const uint4 m12 = R.ld4(CW_M + 2);
                     const double fn1 = (double)(float)(n - 1), fn = (double)(float)n;   // kernel.cu:551-552
                     const double x0 = dbl(a2m0.z, a2m0.w) * fn1, x1 = dbl(m12.x, m12.y) * fn1,
@@ -1262,11 +1271,16 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                         m1 = x1 / fn + acc.g / fn;
                         m2 = x2 / fn + acc.b / fn;
                     }
-                    if (n >= a.spp) {
-                        float* o3 = a.out + out_pixel(a, px, py) * 3;
-                        o3[0] = (float)m0;
-                        o3[1] = (float)m1;
-                        o3[2] = (float)m2;
+                    if ((uint32_t)n >= nend) {   // (a whole pixel's unit ends at spp)
+                        if (fl & CF_CHUNK0) {
+                            double* P = a.lbuf + (size_t)c8.w * 3;
+                            P[0] = m0; P[1] = m1; P[2] = m2;
+                        } else {
+                            float* o3 = a.out + out_pixel(a, px, py) * 3;
+                            o3[0] = (float)m0;
+                            o3[1] = (float)m1;
+                            o3[2] = (float)m2;
+                        }
                         state = ST_IDLE;
                         break;
                     }
@@ -1409,7 +1423,7 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                                         a.pix_states[(UW_CD + 2) * N + u], a.pix_states[UW_TQ * N + u]);
                         R.st4(CW_CD, c8.x, c8.y, c8.z, c8.w);
                     }
-                    if (split) fl |= CF_SPLIT;
+                    if (split) fl |= (n == 1) ? CF_SPLIT | CF_CHUNK0 : CF_SPLIT;
                     if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
                         fl |= (n == 1) ? CF_OWNER : CF_SHARE;   // (chunk 0 starts at sample 1)
                     R.st2(CW_PX, px, py);
