@@ -3211,8 +3211,10 @@ int pt_render_device_async(pt_ctx* c, const pt_params* p, const pt_camera* cam, 
             // (measured on C3 shards: 1/4 shard 3 mid chunks, 1/8 shard 6: +3..4% over one split)
             const uint32_t nfine = (uint32_t)std::min<uint64_t>(b.npix, (uint64_t)(c->wf_fine_px * (double)lanes));
             int mc = c->wf_mid_chunks;
-            if (mc < 0 && nfine < b.npix)   // automatic: ~2.5 mid units per lane, at most 4 chunks
-                mc = std::min(4, (int)std::ceil(2.5 * (double)lanes / (double)(b.npix - nfine)));
+            if (mc < 0 && nfine < b.npix)   // automatic: ~2.5 mid units per lane, at most 3 chunks
+                // (round 5, sample-major split radiance: 3 against 4 at the 1/8 shard, C3 +0.9%, C4 +0.8%,
+                // profiles/r05_mid)
+                mc = std::min(3, (int)std::ceil(2.5 * (double)lanes / (double)(b.npix - nfine)));
             if (mc > 1 && nfine < b.npix) {
                 nmid = b.npix - nfine;
                 chunks_mid = (uint32_t)std::min(mc, p->spp);
