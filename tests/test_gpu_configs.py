@@ -99,6 +99,28 @@ def test_c4_standin_1080p_1024spp_eight_shards_sum_to_full_frame(standin):
     _check(s, full, cam_kw, w, h, spp, 3, _spread(w, h, 2048, 3))
 
 
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_c3_standin_shards_sum_to_full_frame(standin, nshards):
+    """C3 as the 2- and 4-GPU jobs partition it: the half shard splits a tail of its pixels, the quarter
+    shard (1.58 pixels per lane) renders whole pixels for half its lanes and splits the rest into three
+    grades (round 5) -- summed, bit-identical to the full frame."""
+    s, r = standin
+    w, h, spp = 1920, 1080, 256
+    cam = pt.make_camera(width=w, height=h, **scenes.SPONZA_STANDIN_CAMERA)
+    full, st = r.render(cam, w, h, spp, bounces=3)
+    acc = np.zeros_like(full)
+    samples = 0
+    for k in range(nshards):
+        part, sk = r.render(cam, w, h, spp, bounces=3, shard_index=k, shard_count=nshards)
+        mask = np.zeros(w * h, dtype=bool)
+        mask[shard.shard_pixels(w, h, k, nshards)] = True
+        assert np.all(part.reshape(-1, 3)[~mask] == 0)
+        samples += sk["samples"]
+        acc += part
+    assert samples == w * h * spp
+    assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+
+
 def test_c3_fast_walk_equals_reference_walk_full_frame(standin):
     """Every pixel of C3: the measured wavefront kernel (BVH4 walk, culling, winner check, memo,
     dead-path skip, split units) equals the tile kernel walking the reference BVH in the
