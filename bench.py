@@ -332,6 +332,55 @@ def make_reduce(dist, backend, rank):
     return gloo_reduce
 
 
+def make_gather(dist, backend, rank, world, width, height):
+    """The framebuffer's assembly as a gather instead of a reduce: each rank sends only its own tiles' pixels
+    (1/N of the image: 3.1 MB of C3's 24.9 MB at N = 8) to rank 0, which copies them into its framebuffer.  Over
+    xGMI every rank has its own link to rank 0, so the N - 1 transfers run side by side, where a reduce moves the
+    whole framebuffer through the ring.  The result is the same image (every pixel is exactly one rank's value;
+    the reduce adds zeros to it).  RCCL: async (point-to-point sends and receives in one group), the copy into
+    rank 0's framebuffer issued at wait(); gloo: synchronous through host memory."""
+    import torch
+    from cudapathtracer_amd import shard
+    pix = [torch.from_numpy(shard.shard_pixels(width, height, j, world).astype(np.int64)) for j in range(world)]
+    n = max(len(p) for p in pix)
+    slots = {}   # per framebuffer: (device index tensors, send buffer, receive buffers): two frames may be in flight
+
+    def buffers(buf):
+        key = buf.data_ptr()
+        if key not in slots:
+            idx = [p.to(buf.device) for p in pix]
+            send = torch.zeros((n, 3), dtype=buf.dtype, device=buf.device)
+            recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+            slots[key] = (idx, send, recv)
+        return slots[key]
+
+    def unpack(flat, idx, recv):
+        for j in range(1, world):
+            flat.index_copy_(0, idx[j], recv[j][:len(idx[j])].to(flat.device))
+
+    def gather(buf):
+        idx, send, recv = buffers(buf)
+        flat = buf.view(-1, 3)
+        mine = idx[rank]
+        torch.index_select(flat, 0, mine, out=send[:len(mine)])
+        if backend == "nccl":
+            work = dist.gather(send, recv, dst=0, async_op=True)
+
+            class Work:
+                def wait(self_inner):
+                    work.wait()
+                    if rank == 0:
+                        unpack(flat, idx, recv)
+            return Work()
+        host = send.cpu()
+        hrecv = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+        dist.gather(host, hrecv, dst=0)
+        if rank == 0:
+            unpack(flat, idx, hrecv)
+        return None
+    return gather
+
+
 class stdout_to_stderr:
     """Route file descriptor 1 to stderr for the block: the process-group setup's own banners (RCCL's
     version lines, gloo's peer messages) are printed by C++ to stdout, which must carry rank 0's one
@@ -388,6 +437,9 @@ def main():
                     help="frames queued back to back on one stream even for shards (no overlap of consecutive frames)")
     ap.add_argument("--two-streams", action="store_true",
                     help="frames on two streams even for the whole frame (default only for shards of N > 1)")
+    ap.add_argument("--collective", default="reduce", choices=["reduce", "gather"],
+                    help="N > 1: assemble rank 0's image by a reduce of the zero-filled framebuffers (default) or by a "
+                         "gather of each rank's own tiles (1/N of the bytes per rank, point to point)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()
@@ -447,7 +499,9 @@ def main():
                               flags=args.flags, shard_index=rank, shard_count=shards,
                               stream_ptr=torch.cuda.current_stream().cuda_stream)
 
-    red = make_reduce(dist, backend, rank) if distributed else None
+    red = None
+    if distributed:
+        red = make_reduce(dist, backend, rank) if args.collective == "reduce" else make_gather(dist, backend, rank, world, W, H)
     if args.sync_frames:
         loop = FrameLoop(fbs, render, red)
     else:
@@ -514,7 +568,7 @@ def main():
                 args.config, scene_name, W, H, args.spp, args.bounces, args.integrator),
                 "scene": scene_name, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "integrator": "unidirectional" if args.integrator == 0 else "head", "seed": 1234,
-                "parallelism": ("image tiles %dx, %s reduce" % (world, "RCCL" if backend == "nccl" else backend)
+                "parallelism": ("image tiles %dx, %s %s" % (world, "RCCL" if backend == "nccl" else backend, args.collective)
                                 if distributed else
                                 "1 GPU" if shards == 1 else "1 GPU rendering shard 0 of %d (diagnostic)" % shards)},
             "mrays_per_s_traced": round(traced / elapsed / 1e6, 3),

@@ -107,7 +107,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, frames, outdir, asynchronous=False):
+def _worker(rank, world, port, frames, outdir, asynchronous=False, collective="reduce"):
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
     import bench as b
@@ -116,11 +116,12 @@ def _worker(rank, world, port, frames, outdir, asynchronous=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     counter = [0]
     bufs = [torch.zeros((H, W, 3)) for _ in range(2)]
+    red = b.make_reduce(dist, "gloo", rank) if collective == "reduce" else b.make_gather(dist, "gloo", rank, world, W, H)
     if asynchronous:
         enqueue, wait = async_stub(stub_render(rank, world, counter))
-        loop = b.FrameLoop(bufs, enqueue, b.make_reduce(dist, "gloo", rank), wait=wait)
+        loop = b.FrameLoop(bufs, enqueue, red, wait=wait)
     else:
-        loop = b.FrameLoop(bufs, stub_render(rank, world, counter), b.make_reduce(dist, "gloo", rank))
+        loop = b.FrameLoop(bufs, stub_render(rank, world, counter), red)
     stats = [loop.step() for _ in range(frames)]
     fb, rest = loop.drain()
     stats = [st for st in stats if st is not None] + rest
@@ -134,10 +135,11 @@ def _worker(rank, world, port, frames, outdir, asynchronous=False):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,asynchronous", [(2, False), (3, False), (2, True)])
-def test_gloo_frame_loop_assembles_every_frame(tmp_path, world, asynchronous):
+@pytest.mark.parametrize("world,asynchronous,collective", [(2, False, "reduce"), (3, False, "reduce"), (2, True, "reduce"),
+                                                           (2, False, "gather"), (3, True, "gather")])
+def test_gloo_frame_loop_assembles_every_frame(tmp_path, world, asynchronous, collective):
     frames = 3
-    mp.spawn(_worker, args=(world, _free_port(), frames, str(tmp_path), asynchronous), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), frames, str(tmp_path), asynchronous, collective), nprocs=world, join=True)
     fb = np.load(str(tmp_path / "fb.npy"))
     np.testing.assert_array_equal(fb, frame_image(frames - 1))
     tot = np.load(str(tmp_path / "tot.npy"))
