@@ -171,6 +171,9 @@ def roofline(counts, kms, W, H, args, world):
     config -- over this run's kernel time; null otherwise.  binding: the pipes that actually limit the
     kernel, from the same profile.  (The algorithmic bytes are cache_roofline's, against the L2 roof.)"""
     sec = kms * 1e-3
+    # bound: the resource the profile names as binding (binding.limiter); "hbm" only while no profile of this
+    # kernel says otherwise.  achieved / peak / frac / traffic stay the HBM-side figures (also under
+    # hbm_upper_bound): the one roof this pointer-chasing kernel is priced against, an upper bound on HBM bytes.
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
             "traffic_source": None,
             "kernel": KERNEL_NAME(args),
@@ -196,8 +199,14 @@ def roofline(counts, kms, W, H, args, world):
         roof["frac"] = round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4)
         roof["traffic_source"] = {"profile": tj.get("profile"), "method": tj.get("method"),
                                   "kernel_ms_profiled": tj.get("kernel_ms")}
+        roof["hbm_upper_bound"] = {
+            "achieved": roof["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": roof["frac"], "traffic": traffic,
+            "note": "memory-side bytes (L2 misses, Infinity-Cache hits included) per launch over the kernel time: the "
+                    "HBM roof's utilisation at most; not what binds the kernel (see bound / binding)"}
         if tj.get("binding"):
             roof["binding"] = tj["binding"]
+            if roof["binding"].get("limiter"):
+                roof["bound"] = roof["binding"]["limiter"]
         dr = tj.get("dram_requests")
         if dr:
             roof["hbm_counter"] = {
@@ -406,6 +415,70 @@ class stdout_to_stderr:
         return False
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without initialising the GPU (on this image
+    `torch.cuda.device_count()` does not create a HIP context)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, backend, argv=None):
+    """`bench.py --gpus N` with no launcher (WORLD_SIZE unset): start N fresh rank processes of this
+    script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, exactly what
+    `torch.distributed.run` would give them, and relay rank 0's one JSON line.  This parent never touches
+    the GPU (it only counts devices) and never execs: the ranks are children, and it exits with the first
+    failing rank's status (the others are then stopped by PID).  RCCL needs one device per rank, so N larger
+    than the visible GPUs fails loudly; PT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the ranks'
+    device index wraps, as under torch.distributed.run).  Returns the exit status."""
+    import subprocess
+    ndev = visible_gpus()
+    if backend == "nccl" and n > ndev:
+        log("error: --gpus %d but %d GPU(s) visible; RCCL needs one GPU per rank (no fallback to fewer GPUs; "
+            "PT_BENCH_BACKEND=gloo rehearses several ranks on one GPU)" % (n, ndev))
+        return 2
+    argv = list(sys.argv[1:] if argv is None else argv)
+    port = _free_port()
+    procs = []
+    for k in range(n):
+        env = dict(os.environ, RANK=str(k), LOCAL_RANK=str(k), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PT_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if k == 0 else sys.stderr.fileno()))
+    log("launched %d rank processes (%s, 127.0.0.1:%d): pids %s"
+        % (n, backend, port, " ".join(str(p.pid) for p in procs)))
+    import threading
+    out = []   # rank 0's stdout (its one JSON line), read to EOF beside the wait so the pipe cannot fill
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    status = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                log("rank pid %d exited with %d; stopping the other ranks" % (p.pid, rc))
+                for q in pending:
+                    q.kill()
+        if pending:
+            time.sleep(0.05)
+    reader.join()
+    if status == 0:
+        sys.stdout.write(b"".join(out).decode())
+        sys.stdout.flush()
+    return status
+
+
 def KERNEL_NAME(args):
     if args.flags & 1:   # PT_FLAG_REFERENCE_TRAVERSAL: the tile kernel
         return "render_tiles"
@@ -446,6 +519,14 @@ def main():
     for k, v in CONFIGS[args.config].items():
         if k != "scene" and getattr(args, k) is None:
             setattr(args, k, v)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    # PT_BENCH_BACKEND=gloo rehearses the multi-process path where RCCL cannot run (several ranks
+    # on one GPU: the device index wraps over the visible GPUs when there are fewer than ranks)
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # a plain `python bench.py --gpus N`: this process becomes the launcher of N rank processes
+        sys.exit(launch_ranks(args.gpus, backend))
 
     import torch
     import torch.distributed as dist
@@ -459,11 +540,13 @@ def main():
     if world != args.gpus:
         log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
     distributed = world > 1
-    # PT_BENCH_BACKEND=gloo rehearses the multi-process path where RCCL cannot run (several ranks
-    # on one GPU: the device index wraps over the visible GPUs when there are fewer than ranks)
-    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
-    if ndev and local >= ndev:
+    if ndev == 0:
+        raise SystemExit("bench.py: no GPU visible (the render path is HIP only)")
+    if local >= ndev:
+        if backend == "nccl" and distributed:
+            raise SystemExit("bench.py: rank %d has LOCAL_RANK %d but %d GPU(s) are visible; RCCL needs one GPU per "
+                             "rank (PT_BENCH_BACKEND=gloo rehearses several ranks on one GPU)" % (rank, local, ndev))
         local = local % ndev
     torch.cuda.set_device(local)
     if distributed:
@@ -570,7 +653,10 @@ def main():
                 "integrator": "unidirectional" if args.integrator == 0 else "head", "seed": 1234,
                 "parallelism": ("image tiles %dx, %s %s" % (world, "RCCL" if backend == "nccl" else backend, args.collective)
                                 if distributed else
-                                "1 GPU" if shards == 1 else "1 GPU rendering shard 0 of %d (diagnostic)" % shards)},
+                                "1 GPU" if shards == 1 else "1 GPU rendering shard 0 of %d (diagnostic)" % shards),
+                "rank_launcher": (None if not distributed else
+                                  "bench.py (one child process per rank)" if os.environ.get("PT_BENCH_LAUNCHED")
+                                  else "external (WORLD_SIZE set, e.g. torch.distributed.run)")},
             "mrays_per_s_traced": round(traced / elapsed / 1e6, 3),
             "reference_equiv_not_traced": {
                 "mrays_per_s": round(refrays / elapsed / 1e6, 3),

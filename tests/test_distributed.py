@@ -158,3 +158,27 @@ def test_gpu_two_rank_libptamd_shards_reduce_to_full_frame(tmp_path):
             mine[shard.shard_pixels(w, h, k, world)] = True
             assert not np.any(sh[~mine]), (integ, k)
             assert sh[mine].view(np.uint32).tobytes() == full.reshape(-1, 3)[mine].view(np.uint32).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_gpu_plain_bench_gpus2_launches_its_own_ranks():
+    """a plain `bench.py --gpus 2` (no torch.distributed.run, WORLD_SIZE unset) starts two
+    rank processes itself and prints rank 0's one JSON line with n_gpus 2 and a finite image.  On the 1-GPU box
+    the two ranks share GPU 0 over gloo (PT_BENCH_BACKEND=gloo; RCCL refuses two ranks on one device): the same
+    launcher, FrameLoop, shard and reduce path the 8-GPU run takes with RCCL."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PT_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=380)
+    sys.stderr.write(r.stderr[-3000:])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["image_finite"] is True
+    assert d["config"]["rank_launcher"].startswith("bench.py")
+    assert d["value"] > 0 and d["steps"] == 1
