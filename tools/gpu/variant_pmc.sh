@@ -8,7 +8,7 @@ mkdir -p $OUT
 V=variants/${VARIANT:?}/libptamd.so
 for lib in "$V" ""; do
   tag=$([ -n "$lib" ] && echo var || echo base)
-  PT_LIB=$lib timeout -k 10 300 rocprofv3 --pmc TD_TD_BUSY_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVE_CYCLES \
+  PT_LIB=$lib timeout -k 10 300 rocprofv3 --pmc ${PMC:-TD_TD_BUSY_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD} \
       --kernel-trace --output-format csv -d $OUT/pmc_$tag -o run -- \
       python3 bench.py --steps 1 --warmup 0 --no-count --no-cpu-baseline --one-stream > $OUT/pmc_$tag.json 2> $OUT/pmc_$tag.err \
       || { echo "pmc-fail $tag" > $OUT/done.txt; exit 1; }
