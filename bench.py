@@ -512,7 +512,8 @@ def main():
                     help="frames on two streams even for the whole frame (default only for shards of N > 1)")
     ap.add_argument("--collective", default="reduce", choices=["reduce", "gather"],
                     help="N > 1: assemble rank 0's image by a reduce of the zero-filled framebuffers (default) or by a "
-                         "gather of each rank's own tiles (1/N of the bytes per rank, point to point)")
+                         "gather of each rank's own tiles (1/N of the bytes per rank, point to point; rehearsal option: "
+                         "run over gloo on one GPU and as a one-rank RCCL group, never yet on two devices)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--cache-dir", default=os.path.join(tempfile.gettempdir(), "pt_bench_scene"))
     args = ap.parse_args()

@@ -736,6 +736,13 @@ __device__ __forceinline__ uint32_t chunk_first(const Args& a, uint32_t c, uint3
 {
     return (uint32_t)(((uint64_t)c * (uint32_t)a.spp) / chunks);
 }
+// The chunk count of split slot t (its grade: the first nmid slots mid, the last nfin final, the rest fine) -- the one
+// definition init_pixel_states (which deals the chunks), the render kernel (CF_CHUNK0's end) and finalize_pixels
+// (which continues chunk 0's running mean from sample chunk_first(1) on) share.
+__device__ __forceinline__ uint32_t slot_chunks(const Args& a, uint32_t t)
+{
+    return t < a.nmid ? a.chunks_mid : t >= a.ntail - a.nfin ? a.chunks_fin : a.chunks;
+}
 
 // The XORWOW draws one sample of radianceAlongSingleStep2 consumes, without tracing: the count
 // depends only on the draws themselves (lens pair; per bounce u, then 2 for a cosine direction or
@@ -778,7 +785,7 @@ __global__ __launch_bounds__(256) void init_pixel_states(Args a, uint32_t* __res
     const bool mid = split && t < a.nmid;
     const uint32_t f0 = a.ntail - a.nfin;   // first slot of the final grade
     const bool fin = split && t >= f0;
-    const uint32_t nc = !split ? 1u : mid ? a.chunks_mid : fin ? a.chunks_fin : a.chunks;
+    const uint32_t nc = split ? slot_chunks(a, t) : 1u;
     auto unit = [&](uint32_t c) -> size_t {
         if (!split) return (size_t)q;
         if (mid) return (size_t)a.nwhole + (size_t)c * a.nmid + t;
@@ -882,8 +889,7 @@ __global__ __launch_bounds__(256) void finalize_pixels(Args a)
     const size_t stride = (size_t)a.ntail * 3;   // one sample of every slot
     // integrator 0: chunk 0 left its running mean after samples 1..e0 in the sample-1 row (CF_CHUNK0);
     // integrator 1 stores every sample (its chunk 0 keeping the mean measured -1% on the 1/8 shard)
-    const uint32_t nc = t < a.nmid ? a.chunks_mid : t >= a.ntail - a.nfin ? a.chunks_fin : a.chunks;
-    const uint32_t e0 = a.head ? 0u : chunk_first(a, 1u, nc);
+    const uint32_t e0 = a.head ? 0u : chunk_first(a, 1u, slot_chunks(a, t));
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
     if (e0 != 0u) { m0 = L[0]; m1 = L[1]; m2 = L[2]; }
     L += (size_t)e0 * stride;
@@ -1424,6 +1430,11 @@ __device__ __forceinline__ void shade_lane(const Args& a_in, const ColdRec& R, i
                         R.st4(CW_CD, c8.x, c8.y, c8.z, c8.w);
                     }
                     if (split) fl |= (n == 1) ? CF_SPLIT | CF_CHUNK0 : CF_SPLIT;
+#ifdef PT_DEBUG_CHECKS
+                    // finalize_pixels continues a CF_CHUNK0 slot's mean from sample chunk_first(1): the unit must end there
+                    if (split && n == 1 && nend != chunk_first(a, 1u, slot_chunks(a, a.pix_states[UW_TQ * N + u])))
+                        __builtin_trap();
+#endif
                     if (split && !(fl & CF_LENS) && !(a.flags & PT_FLAG_NO_PRIMARY_CACHE))
                         fl |= (n == 1) ? CF_OWNER : CF_SHARE;   // (chunk 0 starts at sample 1)
                     R.st2(CW_PX, px, py);

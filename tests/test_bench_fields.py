@@ -105,9 +105,9 @@ def test_roofline_bound_names_the_binding_limiter(tmp_path):
     p.write_text(json.dumps({"entries": [{"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha,
                                           "traffic_bytes_per_launch": 343_000_000_000, "kernel_ms": 90.0,
                                           "profile": "profiles/x",
-                                          "binding": {"limiter": "walk_memory_round_trips", "limiter_detail": "..."}}]}))
+                                          "binding": {"limiter": "walk_steps_x_step_valu", "limiter_detail": "..."}}]}))
     roof = bench.roofline(COUNTS, 90.0, 1920, 1080, _args(str(p)), 1)
-    assert roof["bound"] == roof["binding"]["limiter"] == "walk_memory_round_trips"
+    assert roof["bound"] == roof["binding"]["limiter"] == "walk_steps_x_step_valu"
     h = roof["hbm_upper_bound"]
     assert h["frac"] == roof["frac"] and h["achieved"] == roof["achieved"] and h["traffic"] == roof["traffic"]
     assert h["achieved"] <= h["peak"] == bench.HBM_PEAK_GBS
@@ -119,7 +119,7 @@ def test_committed_profiles_name_a_limiter():
     for e in tj["entries"]:
         b = e.get("binding")
         if b:
-            assert b["limiter"] in ("walk_memory_round_trips", "lds_walk_and_f64_shading_issue"), e["config"]
+            assert b["limiter"] in ("walk_steps_x_step_valu", "lds_walk_and_f64_shading_issue"), e["config"]
             assert len(b["limiter_detail"]) > 40
 
 

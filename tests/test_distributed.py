@@ -182,3 +182,46 @@ def test_gpu_plain_bench_gpus2_launches_its_own_ranks():
     assert d["n_gpus"] == 2 and d["image_finite"] is True
     assert d["config"]["rank_launcher"].startswith("bench.py")
     assert d["value"] > 0 and d["steps"] == 1
+
+
+_NCCL_WORLD1 = r'''
+import os, sys, json
+sys.path.insert(0, %r)
+import numpy as np
+import torch
+import torch.distributed as dist
+import bench
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d", device_id=torch.device("cuda", 0))
+W, H = 40, 24
+out = {}
+for kind in ("reduce", "gather"):
+    fn = bench.make_reduce(dist, "nccl", 0) if kind == "reduce" else bench.make_gather(dist, "nccl", 0, 1, W, H)
+    buf = torch.arange(H * W * 3, dtype=torch.float32, device="cuda").reshape(H, W, 3) / 7.0
+    ref = buf.clone()
+    work = fn(buf)
+    assert work is not None          # RCCL: asynchronous
+    work.wait()
+    torch.cuda.synchronize()
+    out[kind] = bool(torch.equal(buf, ref))
+dist.destroy_process_group()
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(200)
+def test_gpu_rccl_reduce_and_gather_world1():
+    """ADVICE r05: bench.py's RCCL legs (make_reduce's async reduce, make_gather's async gather with the unpack done at
+    wait()) run on a CUDA tensor in a one-rank RCCL group -- the asynchronous Work.wait() path the 8-GPU run takes --
+    and leave rank 0's framebuffer exactly as rendered (with one rank the gather unpacks nothing and the reduce adds
+    nothing).  Multi-device behaviour stays unmeasured here (1-GPU boxes)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", _NCCL_WORLD1 % (ROOT, _free_port())], env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res == {"reduce": True, "gather": True}

@@ -42,17 +42,21 @@ if "GRBM_GUI_ACTIVE" in c:
     if cfg[:4] == [1024, 1024, 64, 8]:   # C2: the 32-triangle Cornell tree, held whole in LDS
         lim = ("C2's tree (32 triangles) is read from LDS and every other record hits L2: not bytes -- the path "
                "state held in registers removed 37-42% of the memory-side bytes for -0.8% (profiles/r04_c2_regstate); "
-               "the walk runs at SIMD utilisation ~0.39 (walk threshold 62, LDS round trips per step) and the f64 "
-               "shading pass carries most of the VALU, whose issue rate below is about half the wave64 ceiling; "
-               "TD_TC_STALL is the vector memory's share of cycles stalled on the record's L2 round trips (DESIGN.md 6)")
+               "the walk (56% of the wave-clock, SIMD utilisation ~0.39 at walk threshold 62) is bound by the VALU it "
+               "issues, not by its phase structure or LDS round trips -- an exhaustive LDS trace with no walk phase and "
+               "12x the triangle tests lost 20% (profiles/r06_exhaustive); the f64 shading pass (44%) spreads over "
+               "sampling, sample ends, trace begins and dead-path replays with none dominant (profiles/r06_sections); "
+               "VALU issue about half the wave64 ceiling (DESIGN.md 6.3)")
     else:
-        lim = ("the walk's dependent memory round trips per ray (walk steps) and their latency: the step's dependent "
-               "VALU (deferred under the next fetch: +-0), its L1 lookups (-18%: +-0; -21% / -37% by the cooperative "
-               "fetch, which lengthens the chain: -7% / -16%, profiles/r05_coop) and a sixth wave per SIMD each left "
-               "the rate unchanged or lower, fewer steps moved it (DESIGN.md 6, 10); TD busy counts requests in "
-               "flight, VALU issue is about half its wave64 rate (0.5 wave64 instructions per SIMD-cycle)")
+        lim = ("the walk's steps per ray times the VALU each step issues (~200 per wave-step, the wave paying all 64 "
+               "lanes' slots): fewer steps per ray paid every time (margin test, leaves of 2, light probe, DP collapse, "
+               "DESIGN_LOG 6); removing vector-memory loads from the step did not (round 6: 1 and 2 of 10 loads removed "
+               "with +3.7% and +12% dynamic VALU -> -3.9% and -7.0%, cycles following the VALU at an unchanged issue "
+               "rate, profiles/r06_fold, r06_qnode), nor did fewer L1 lookups (-18..-37%: +-0 or worse), fewer memory-"
+               "side bytes (-11.5%: +0.3%) or a sixth wave; TD busy ~0.99 counts requests in flight, VALU issue is "
+               "about half its wave64 rate")
     # limiter: the binding resource as one key (bench.py's roofline.bound); limiter_detail: the evidence
-    kind = "lds_walk_and_f64_shading_issue" if cfg[:4] == [1024, 1024, 64, 8] else "walk_memory_round_trips"
+    kind = "lds_walk_and_f64_shading_issue" if cfg[:4] == [1024, 1024, 64, 8] else "walk_steps_x_step_valu"
     b = {"limiter": kind, "limiter_detail": lim, "cycles_per_launch": int(cyc)}
     if "SQ_INSTS_VALU" in c:
         # wave64 VALU instructions per SIMD-cycle; the issue ceiling is 0.5 (a wave64 VALU instruction
