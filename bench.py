@@ -207,6 +207,17 @@ def roofline(counts, kms, W, H, args, world):
             roof["binding"] = tj["binding"]
             if roof["binding"].get("limiter"):
                 roof["bound"] = roof["binding"]["limiter"]
+            vi = roof["binding"].get("valu_issue_ms_per_launch")
+            if vi:
+                # the binding roof: the launch's VALU instructions priced at the rate the kernel's own streams
+                # issue at alone (profiles/r06_valu, tools/valu_bound.py) against this run's kernel time
+                roof["valu_issue"] = {
+                    "achieved_ms": vi, "kernel_ms": round(kms, 3), "frac": round(vi / kms, 4), "unit": "ms per launch",
+                    "method": roof["binding"].get("valu_issue_method"),
+                    "note": "the time the SIMDs need just to issue this launch's VALU instructions (counted by "
+                            "SQ_INSTS_VALU in the profile of this kernel source and config) at the rate the kernel's own "
+                            "walk / shading instruction streams reach replayed alone at 5 waves per SIMD; frac ~1 means "
+                            "VALU issue fills the launch and memory latency is hidden (DESIGN.md 6.3)"}
         dr = tj.get("dram_requests")
         if dr:
             roof["hbm_counter"] = {

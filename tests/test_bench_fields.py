@@ -119,8 +119,39 @@ def test_committed_profiles_name_a_limiter():
     for e in tj["entries"]:
         b = e.get("binding")
         if b:
-            assert b["limiter"] in ("walk_steps_x_step_valu", "lds_walk_and_f64_shading_issue"), e["config"]
+            assert b["limiter"] in ("valu_issue", "walk_steps_x_step_valu", "lds_walk_and_f64_shading_issue"), e["config"]
             assert len(b["limiter_detail"]) > 40
+            if b["limiter"] == "valu_issue":   # priced: the VALU issue time of the launch, near its duration
+                assert 0.8 < b["valu_issue_frac_profiled"] < 1.1, e["config"]
+
+
+def test_valu_issue_block(tmp_path):
+    """A profile that prices the launch's VALU issue (tools/valu_bound.py) gives the bench line a valu_issue block
+    over this run's kernel time, and bound names it."""
+    sha = bench.kernel_source_sha256()
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps({"entries": [{"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha,
+                                          "traffic_bytes_per_launch": 343_000_000_000, "kernel_ms": 90.0,
+                                          "profile": "profiles/x",
+                                          "binding": {"limiter": "valu_issue", "limiter_detail": "...",
+                                                      "valu_issue_ms_per_launch": 88.0,
+                                                      "valu_issue_method": "m"}}]}))
+    roof = bench.roofline(COUNTS, 90.0, 1920, 1080, _args(str(p)), 1)
+    assert roof["bound"] == "valu_issue"
+    assert roof["valu_issue"]["frac"] == round(88.0 / 90.0, 4) and roof["valu_issue"]["kernel_ms"] == 90.0
+
+
+def test_valu_bound_tool_reproduces_the_committed_pricing():
+    """tools/valu_bound.py on the committed replay rates, section counts and C3 profile gives the blend that
+    profiles/r06_valu/valu_bound.json (and so traffic.json) carries."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("valu_bound", os.path.join(bench.ROOT, "tools", "valu_bound.py"))
+    vb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(vb)
+    r = vb.bound(os.path.join(bench.ROOT, "profiles", "r06_final", "pmc_summary.json"))
+    ref = json.load(open(os.path.join(bench.ROOT, "profiles", "r06_valu", "valu_bound.json")))
+    assert r["cycles_per_valu_blend"] == ref["cycles_per_valu_blend"]
+    assert 3.0 < r["cycles_per_valu_walk_replay"] < 5.0 and 3.0 < r["cycles_per_valu_shading_replay"] < 5.0
 
 
 def test_plain_multi_gpu_bench_fails_loudly_without_enough_gpus():

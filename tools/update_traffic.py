@@ -46,21 +46,44 @@ if "GRBM_GUI_ACTIVE" in c:
                "issues, not by its phase structure or LDS round trips -- an exhaustive LDS trace with no walk phase and "
                "12x the triangle tests lost 20% (profiles/r06_exhaustive); the f64 shading pass (44%) spreads over "
                "sampling, sample ends, trace begins and dead-path replays with none dominant (profiles/r06_sections); "
-               "VALU issue about half the wave64 ceiling (DESIGN.md 6.3)")
+               "VALU issue 0.276 per SIMD-cycle, the rate at which integrator 0's replayed streams fill every issue "
+               "cycle (DESIGN.md 6.3; C2's own LDS-walk stream is not replayed)")
     else:
         lim = ("the walk's steps per ray times the VALU each step issues (~200 per wave-step, the wave paying all 64 "
                "lanes' slots): fewer steps per ray paid every time (margin test, leaves of 2, light probe, DP collapse, "
                "DESIGN_LOG 6); removing vector-memory loads from the step did not (round 6: 1 and 2 of 10 loads removed "
                "with +3.7% and +12% dynamic VALU -> -3.9% and -7.0%, cycles following the VALU at an unchanged issue "
                "rate, profiles/r06_fold, r06_qnode), nor did fewer L1 lookups (-18..-37%: +-0 or worse), fewer memory-"
-               "side bytes (-11.5%: +0.3%) or a sixth wave; TD busy ~0.99 counts requests in flight, VALU issue is "
-               "about half its wave64 rate")
+               "side bytes (-11.5%: +0.3%) or a sixth wave; TD busy ~0.99 counts requests in flight; VALU issue "
+               "~0.26 per SIMD-cycle, at which integrator 0's replayed streams fill every issue cycle (DESIGN.md 6.3)")
     # limiter: the binding resource as one key (bench.py's roofline.bound); limiter_detail: the evidence
     kind = "lds_walk_and_f64_shading_issue" if cfg[:4] == [1024, 1024, 64, 8] else "walk_steps_x_step_valu"
+    # the integrator-0 kernel on the stand-in: its VALU priced at the rate its own streams issue at alone
+    # (profiles/r06_valu, tools/valu_bound.py) -- the VALU issue time of the launch against its duration
+    vb_path = os.path.join(ROOT, "profiles", "r06_valu", "valu_bound.json")
+    vb = json.load(open(vb_path)) if os.path.exists(vb_path) else None
+    priced = (vb is not None and "SQ_INSTS_VALU" in c and kind == "walk_steps_x_step_valu"
+              and "render_unidir_wf<false, 5, false>" in out["kernel"])
+    if priced:
+        kind = "valu_issue"
+        lim = ("VALU issue: the launch's VALU instructions, priced at the rate the kernel's own instruction streams "
+               "issue at when replayed alone with no memory at 5 waves per SIMD (walk step %.2f, shading %.2f SIMD-"
+               "cycles per instruction; profiles/r06_valu, tools/valu_bound.py), take %s of its time -- the SIMDs "
+               "issue VALU in nearly every cycle and memory latency is hidden. Consistent with every round-6 "
+               "experiment: removing 1-2 of the step's 10 loads at +3.7%%/+12%% VALU lost 3.9%%/7.0%% (r06_fold, "
+               "r06_qnode); fewer L1 lookups or memory-side bytes bought nothing; fewer walk steps per ray always paid"
+               % (vb["cycles_per_valu_walk_replay"], vb["cycles_per_valu_shading_replay"], "%.0f%%"))
     b = {"limiter": kind, "limiter_detail": lim, "cycles_per_launch": int(cyc)}
+    if priced:
+        issue_ms = c["SQ_INSTS_VALU"] / 1024 * vb["cycles_per_valu_blend"] / 2.4e9 * 1e3
+        b["valu_issue_ms_per_launch"] = round(issue_ms, 3)
+        b["valu_issue_frac_profiled"] = round(issue_ms / kms, 4) if kms else None
+        b["valu_issue_method"] = ("SQ_INSTS_VALU / 1024 SIMDs x %.4f SIMD-cycles per instruction (the walk / shading blend "
+                                  "of the replayed streams, weighted as in the C3 launch) at 2.4 GHz" % vb["cycles_per_valu_blend"])
+        b["limiter_detail"] = lim.replace("%.0f%%", "%.0f%%" % (100 * issue_ms / kms) if kms else "most")
     if "SQ_INSTS_VALU" in c:
-        # wave64 VALU instructions per SIMD-cycle; the issue ceiling is 0.5 (a wave64 VALU instruction
-        # issues over 2 cycles on CDNA4's SIMD-32, MI355X_MICROARCH.md "Wave scheduling")
+        # wave64 VALU instructions per SIMD-cycle; measured ceiling ~0.25-0.3 for this kernel's mix (most
+        # classes take 3.9-4.7 SIMD-cycles at >= 2 waves per SIMD, moves 2.3: profiles/r06_valu/valu_cost.txt)
         b["valu_insts_per_simd_cycle"] = round(c["SQ_INSTS_VALU"] / (1024 * cyc), 4)
     if "TD_TD_BUSY_sum" in c:
         b["td_busy"] = round(c["TD_TD_BUSY_sum"] / 256 / cyc, 4)
