@@ -13,4 +13,6 @@ tail -1 $OUT/pytest_gpu.log
 timeout -k 10 600 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo bench-fail > $OUT/done_a.txt; exit 1; }
 echo "bench $(python3 -c "import json;d=json.load(open('$OUT/bench_default.json'));print(d['value'], d['ms_per_step'])")"
 TAG=${TAG:-r06_final}/prof bash tools/gpu/profile.sh || { echo prof-fail > $OUT/done_a.txt; exit 1; }
+# the kernel's own VALU streams replayed alone (tools/gpu/micro/walk_replay, generated from this kernel's ISA)
+timeout -k 10 120 tools/gpu/micro/walk_replay > $OUT/walk_replay.txt 2>&1 || { echo replay-fail > $OUT/done_a.txt; exit 1; }
 echo ok > $OUT/done_a.txt

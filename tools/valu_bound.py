@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIMDS = 1024            # 256 CUs x 4
 REPLAY_CLOCK = 2.4e9    # walk_replay converts its event times to cycles at this clock; undone below
 # static VALU per execution of the replayed shading sections (the PT_SEC_MARKERS listing, profiles/r06_sections)
-STATIC = {"cosine": 428, "sample_end": 214, "begin": 858}
+STATIC = {"cosine": 428, "sample_end": 213, "begin": 852}
 SEC_ORDER = ["PASS", "CHECK", "SLOW", "BOUNCE", "EMIT", "COSINE", "LIGHT", "SAMPLE_END", "START", "CAMERA", "DEAD",
              "BEGIN", "REFILL", "MEMO", "RECORD", "PROBE"]
 

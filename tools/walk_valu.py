@@ -7,7 +7,7 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "cudapathtracer_amd/csrc/build/pt_render.s"
 lines = open(path).read().split("\n")
-start = next(i for i, l in enumerate(lines) if re.match(r"^_ZN12_GLOBAL__N_116render_unidir_wfILb0ELi5EEEvNS_4ArgsE:", l))
+start = next(i for i, l in enumerate(lines) if re.match(r"^_ZN12_GLOBAL__N_116render_unidir_wfILb0ELi5E(Lb0E)?EEvNS_4ArgsE:", l))
 lines = lines[start:]
 h = next(i for i, l in enumerate(lines) if "This Loop Header: Depth=2" in l)
 hdr = re.search(r"^(\.LBB\d+_\d+):", lines[h - 1] if lines[h - 1].startswith(".LBB") else lines[h]).group(1) \
