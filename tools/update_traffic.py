@@ -49,7 +49,7 @@ if "GRBM_GUI_ACTIVE" in c:
                "VALU issue 0.276 per SIMD-cycle, the rate at which integrator 0's replayed streams fill every issue "
                "cycle (DESIGN.md 6.3; C2's own LDS-walk stream is not replayed)")
     else:
-        lim = ("the walk's steps per ray times the VALU each step issues (~200 per wave-step, the wave paying all 64 "
+        lim = ("the walk's steps per ray times the VALU each step issues (~160 per wave-step, the wave paying all 64 "
                "lanes' slots): fewer steps per ray paid every time (margin test, leaves of 2, light probe, DP collapse, "
                "DESIGN_LOG 6); removing vector-memory loads from the step did not (round 6: 1 and 2 of 10 loads removed "
                "with +3.7% and +12% dynamic VALU -> -3.9% and -7.0%, cycles following the VALU at an unchanged issue "
