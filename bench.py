@@ -203,7 +203,18 @@ def roofline(counts, kms, W, H, args, world):
             "achieved": roof["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": roof["frac"], "traffic": traffic,
             "note": "memory-side bytes (L2 misses, Infinity-Cache hits included) per launch over the kernel time: the "
                     "HBM roof's utilisation at most; not what binds the kernel (see bound / binding)"}
-        if tj.get("binding"):
+        binding = tj.get("binding")
+        shards = max(world, args.sim_shards)
+        if not binding and shards > 1:
+            # a shard launch's profile holds its bytes only: the limiter is the full-frame launch's (the same kernel
+            # on 1/N of the tiles), without that launch's per-launch VALU pricing
+            full = traffic_entry(args.traffic_json, [W, H, args.spp, args.bounces, args.integrator, 1],
+                                 roof["kernel_source_sha256"])
+            if full and full.get("binding"):
+                binding = {k: v for k, v in full["binding"].items() if not k.startswith("valu_issue")}
+                binding["inherited_from"] = full.get("profile")
+        if binding:
+            tj = dict(tj, binding=binding)
             roof["binding"] = tj["binding"]
             if roof["binding"].get("limiter"):
                 roof["bound"] = roof["binding"]["limiter"]

@@ -169,3 +169,19 @@ def test_plain_multi_gpu_bench_fails_loudly_without_enough_gpus():
     assert r.returncode != 0
     assert r.stdout == ""                 # no JSON line
     assert "RCCL needs one GPU per rank" in r.stderr
+
+
+def test_shard_launch_inherits_the_full_frame_limiter(tmp_path):
+    """At N > 1 the shard launch's profile holds only its bytes; bound still names the full-frame launch's limiter
+    (same kernel on 1/N of the tiles), without the full frame's per-launch VALU pricing."""
+    sha = bench.kernel_source_sha256()
+    p = tmp_path / "t.json"
+    full = {"config": [1920, 1080, 256, 3, 0, 1], "kernel_source_sha256": sha, "traffic_bytes_per_launch": 343_000_000_000,
+            "kernel_ms": 90.0, "profile": "profiles/full",
+            "binding": {"limiter": "valu_issue", "limiter_detail": "...", "valu_issue_ms_per_launch": 88.0}}
+    shard = {"config": [1920, 1080, 256, 3, 0, 8], "kernel_source_sha256": sha, "traffic_bytes_per_launch": 45_000_000_000,
+             "kernel_ms": 11.7, "profile": "profiles/shard8"}
+    p.write_text(json.dumps({"entries": [full, shard]}))
+    roof = bench.roofline(COUNTS, 11.7, 1920, 1080, _args(str(p)), 8)
+    assert roof["bound"] == "valu_issue" and roof["binding"]["inherited_from"] == "profiles/full"
+    assert "valu_issue" not in roof and "valu_issue_ms_per_launch" not in roof["binding"]
