@@ -132,6 +132,22 @@ SIGNATURES = {
 _lib = None
 
 
+def _torch_runtime_first():
+    """One process, two HIP runtimes: PyTorch's ROCm wheel bundles its own (torch/lib/libamdhip64.so, loaded by path),
+    libptamd.so links the system's (libamdhip64.so.7).  With this library's runtime up first, PyTorch then finds no
+    device ("no ROCm-capable device is detected", profiles/r06_async_dbg); with PyTorch's first, both work (every suite
+    and bench run).  So when PyTorch is importable and sees a GPU, its runtime is initialised before the library is
+    loaded (PT_NO_TORCH_FIRST=1 skips this; the C-ABI itself never needs PyTorch)."""
+    if os.environ.get("PT_NO_TORCH_FIRST"):
+        return
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def lib():
     """Load libptamd.so once; raise loudly if it has not been built."""
     global _lib
@@ -140,6 +156,7 @@ def lib():
             raise RuntimeError(
                 "libptamd.so not found at %s: build it with `python __graft_entry__.py build` "
                 "(there is no fallback render path)" % LIB_PATH)
+        _torch_runtime_first()
         handle = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(handle, name)
