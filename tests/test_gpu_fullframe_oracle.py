@@ -3,8 +3,9 @@
 bit (kernel.cu:417-515 via the oracle's restatement).  The default GPU suite compares pixel subsets at these sizes;
 this covers every pixel.
 
-Opt-in (CPU-heavy): PT_FULL_FRAME=C2,C3,C4 selects the configs (skipped otherwise); PT_FULL_FRAME_LOG=path receives a
-progress line per band of rows and a result line per config.  C3 takes ~2 min of 16 host threads, C4 ~9 min.
+Opt-in (CPU-heavy): PT_FULL_FRAME=C2,C3,C4,C3H selects the configs (C3H: C3 with the HEAD integrator, kernel.cu:217-415;
+skipped otherwise); PT_FULL_FRAME_LOG=path receives a progress line per band of rows and a result line per config.  C3
+takes ~2 min of 16 host threads, C4 ~9 min, C3H ~6 min.
 """
 import json
 import os
@@ -29,7 +30,7 @@ def _log(msg):
             fh.write(msg + "\n")
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C3H"])
 def test_full_frame_matches_the_oracle(cfg, tmp_path):
     if cfg not in SEL:
         pytest.skip("PT_FULL_FRAME does not select %s" % cfg)
@@ -37,7 +38,8 @@ def test_full_frame_matches_the_oracle(cfg, tmp_path):
     import bench
     import oracle
     from cudapathtracer_amd import scenes
-    c = bench.CONFIGS[cfg]
+    integ = 1 if cfg.endswith("H") else 0
+    c = bench.CONFIGS[cfg.rstrip("H")]
     W, H, spp, D = c["width"], c["height"], c["spp"], c["bounces"]
     path, mtl, _ = bench.scene_path(str(tmp_path), c["scene"])
     s = pt.Scene()
@@ -47,7 +49,7 @@ def test_full_frame_matches_the_oracle(cfg, tmp_path):
     with pt.Renderer(s, 0) as r:
         cam = pt.make_camera(width=W, height=H, **cam_kw)
         t0 = time.time()
-        img, st = r.render(cam, W, H, spp, bounces=D)
+        img, st = r.render(cam, W, H, spp, bounces=D, integrator=integ)
         gpu_s = time.time() - t0
     osc = oracle.OracleScene(s.arrays())
     ocam = oracle.camera(cam_kw["pos"], cam_kw["dist_from_film"], cam_kw["focal_length"], cam_kw["radius"], W, H)
@@ -59,13 +61,13 @@ def test_full_frame_matches_the_oracle(cfg, tmp_path):
     for y0 in range(0, H, band):
         y1 = min(H, y0 + band)
         pix = np.arange(y0 * W, y1 * W, dtype=np.uint32)
-        part, cnt = oracle.render(osc, ocam, W, H, spp, D, 0, 1234, pixels=pix, threads=threads)
+        part, cnt = oracle.render(osc, ocam, W, H, spp, D, integ, 1234, pixels=pix, threads=threads)
         ref[y0:y1] = part[y0:y1]
         traces += cnt["traces"]
         _log("%s rows %d-%d done, %.0f s" % (cfg, y0, y1, time.time() - t0))
     cpu_s = time.time() - t0
     diff = int(np.count_nonzero(img.view(np.uint32) != ref.astype(np.float32).view(np.uint32)))
-    _log(json.dumps(dict(config=cfg, width=W, height=H, spp=spp, bounces=D, pixels=W * H, samples=W * H * spp,
+    _log(json.dumps(dict(config=cfg, integrator=integ, width=W, height=H, spp=spp, bounces=D, pixels=W * H, samples=W * H * spp,
                          differing_values=diff, rays_reference_gpu=int(st["rays_reference"]), traces_oracle=int(traces),
                          gpu_render_s=round(gpu_s, 3), oracle_s=round(cpu_s, 1), oracle_threads=threads,
                          nonzero=int(np.count_nonzero(img)))))

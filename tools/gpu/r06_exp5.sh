@@ -3,7 +3,7 @@
 # instructions) against the product, C3 alternated, and one L2 hit/miss pass each.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r06_exp5b
+OUT=gpurun_out/r06_exp5c
 mkdir -p $OUT
 PT_LIB=variants/tri64/libptamd.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_random_scenes.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_tri64.log 2>&1 || { echo pytest-fail; tail -20 $OUT/pytest_tri64.log; exit 1; }
 tail -1 $OUT/pytest_tri64.log
